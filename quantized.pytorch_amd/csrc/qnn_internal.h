@@ -1,0 +1,69 @@
+// Internal helpers shared by the qnn HIP translation units (gfx950 / CDNA4 only).
+//
+// Quantizer arithmetic restates models/modules/quantize.py:89-100 (the effective
+// asymmetric branch) op-for-op in fp32:
+//   t = fl(x + (-min)); u = fl(t / s) (IEEE division); u = clamp(u, 0, qmax);
+//   q = rint(u) (round half to even);  x_hat = fl(fl(q * s) + min).
+// The library is built with -ffp-contract=off so none of these is fused.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/qnn.h"
+
+namespace qnn {
+
+void set_error(const std::string& msg);
+int hip_check(hipError_t e, const char* what);
+int arg_error(const char* what);
+
+#define QNN_REQUIRE(cond, msg) \
+  do {                         \
+    if (!(cond)) return ::qnn::arg_error(msg); \
+  } while (0)
+
+#define QNN_LAUNCH_CHECK(what) \
+  do {                         \
+    hipError_t _e = hipGetLastError(); \
+    if (_e != hipSuccess) return ::qnn::hip_check(_e, what); \
+  } while (0)
+
+// -------------------------------------------------------------- device math
+__device__ __forceinline__ float quant_code(float x, float neg_min, float scale, float qmax) {
+  float t = x + neg_min;           // add_(-min_value)        :90
+  float u = t / scale;             // div_(scale)             :90 (true fp32 division)
+  u = u + 0.0f;                    // add_(qmin)              :90
+  u = fminf(fmaxf(u, 0.0f), qmax); // clamp_(qmin, qmax)      :95
+  return rintf(u);                 // round_()  half-to-even  :95
+}
+
+__device__ __forceinline__ float dequant(float q, float scale, float min) {
+  float v = q * scale;             // add_(-qmin).mul_(scale) :100
+  return v + min;                  // add_(min_value)         :100
+}
+
+__device__ __forceinline__ float fake_quant(float x, float neg_min, float min, float scale, float qmax) {
+  return dequant(quant_code(x, neg_min, scale, qmax), scale, min);
+}
+
+// Wave64 reductions.
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace qnn

@@ -1,0 +1,427 @@
+// Quantizer, weight pre-pack, RangeBN and depthwise kernels of the qnn C ABI.
+// Reference semantics: models/modules/quantize.py (see include/qnn.h per entry).
+#include <stdio.h>
+#include <string.h>
+
+#include "qnn_internal.h"
+
+namespace qnn {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return QNN_OK;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return QNN_ERR_HIP;
+}
+
+int arg_error(const char* what) {
+  set_error(std::string("invalid argument: ") + what);
+  return QNN_ERR_ARG;
+}
+
+// ------------------------------------------------------------------ fake quant
+__global__ void fake_quant_kernel(const float* __restrict__ x, float* y, int64_t n, float neg_min,
+                                  float min, float scale, float qmax) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (; i < n; i += stride) {
+    if (i + 4 <= n && ((((uintptr_t)(x + i)) | ((uintptr_t)(y + i))) & 15) == 0) {
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      v.x = fake_quant(v.x, neg_min, min, scale, qmax);
+      v.y = fake_quant(v.y, neg_min, min, scale, qmax);
+      v.z = fake_quant(v.z, neg_min, min, scale, qmax);
+      v.w = fake_quant(v.w, neg_min, min, scale, qmax);
+      *reinterpret_cast<float4*>(y + i) = v;
+    } else {
+      for (int64_t j = i; j < n && j < i + 4; ++j) y[j] = fake_quant(x[j], neg_min, min, scale, qmax);
+    }
+  }
+}
+
+__global__ void fake_quant_rows_kernel(const float* __restrict__ x, float* y, int rows, int64_t cols,
+                                       const float* __restrict__ mins, const float* __restrict__ maxs, float qmax) {
+  const int r = blockIdx.y;
+  const float mn = mins[r], mx = maxs[r];
+  float s = (mx - mn) / qmax;  // quantize.py:71 (tensor scale, fp32)
+  s = fmaxf(s, 1e-8f);         // :73
+  const float* xr = x + (int64_t)r * cols;
+  float* yr = y + (int64_t)r * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += (int64_t)gridDim.x * blockDim.x)
+    yr[i] = fake_quant(xr[i], -mn, mn, s, qmax);
+}
+
+// One 1024-thread block: range of the vector, then quantize it.
+__global__ __launch_bounds__(1024) void fake_quant_vec_kernel(const float* __restrict__ x, float* y, int n,
+                                                              float qmax, int scale_mode, float* range_out) {
+  __shared__ float smin[16], smax[16];
+  __shared__ float s_params[3];
+  float lo = INFINITY, hi = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float v = x[i];
+    lo = fminf(lo, v);
+    hi = fmaxf(hi, v);
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    smin[wid] = lo;
+    smax[wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int nw = (blockDim.x + 63) >> 6;
+    float mn = smin[0], mx = smax[0];
+    for (int k = 1; k < nw; ++k) {
+      mn = fminf(mn, smin[k]);
+      mx = fmaxf(mx, smax[k]);
+    }
+    float s;
+    if (scale_mode == 0) {
+      s = (mx - mn) / qmax;           // tensor scale (quantize.py:71), fp32
+      s = fmaxf(s, 1e-8f);            // scale.clamp_(1e-8)      (:73)
+    } else {
+      double sd = ((double)mx - (double)mn) / (double)qmax;  // Python float scale (:71)
+      sd = sd > 1e-8 ? sd : 1e-8;                             // max(scale, 1e-8) (:75)
+      s = (float)sd;                                          // cast at div_/mul_
+    }
+    s_params[0] = mn;
+    s_params[1] = mx;
+    s_params[2] = s;
+    if (range_out) {
+      range_out[0] = mn;
+      range_out[1] = mx;
+    }
+  }
+  __syncthreads();
+  float mn = s_params[0], s = s_params[2];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) y[i] = fake_quant(x[i], -mn, mn, s, qmax);
+}
+
+// ------------------------------------------------------------------ NCHW -> NHWC8
+// Each thread: one pixel, 16 channels (one 16-byte output chunk).  Reads are
+// coalesced along the pixel index, writes are 16 B per lane.
+__global__ void quantize_nchw_nhwc8_kernel(const float* __restrict__ x, int8_t* __restrict__ q, int n, int c,
+                                           int hw, int cp, float neg_min, float scale, float qmax) {
+  int64_t npix = (int64_t)n * hw;
+  int groups = cp >> 4;
+  int64_t total = npix * groups;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t pix = idx % npix;
+    int g = (int)(idx / npix);
+    int64_t img = pix / hw;
+    int64_t p = pix - img * hw;
+    const float* src = x + (img * c) * hw + p;
+    union {
+      int8_t b[16];
+      int4 v;
+    } out;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      int ch = g * 16 + j;
+      int8_t code = 0;
+      if (ch < c) code = (int8_t)((int)quant_code(src[(int64_t)ch * hw], neg_min, scale, qmax) - 128);
+      out.b[j] = code;
+    }
+    *reinterpret_cast<int4*>(q + pix * cp + g * 16) = out.v;
+  }
+}
+
+// ------------------------------------------------------------------ weight pack
+// One block per (padded) output channel.  Deterministic fp64 tap sums.
+__global__ __launch_bounds__(256) void pack_weight_kernel(const float* __restrict__ w, int cout, int cin_g, int kh,
+                                                          int kw, int cin_pad, int kpad, float qmax,
+                                                          const float* w_min_in, const float* w_max_in,
+                                                          int8_t* __restrict__ wq, float* s_w, float* b_w,
+                                                          float* tap_sum, float* w_hat, float* w_min_out,
+                                                          float* w_max_out) {
+  const int c = blockIdx.x;
+  const int taps = kh * kw;
+  const int E = cin_g * taps;
+  int8_t* row = wq + (int64_t)c * kpad;
+  if (c >= cout) {
+    for (int i = threadIdx.x; i < kpad; i += blockDim.x) row[i] = 0;
+    return;
+  }
+  __shared__ float s_mm[2][4];
+  __shared__ double s_red[4];
+  const float* wc = w + (int64_t)c * E;
+  float mn, mx;
+  if (w_min_in && w_max_in) {
+    mn = w_min_in[c];
+    mx = w_max_in[c];
+  } else {
+    float lo = INFINITY, hi = -INFINITY;
+    for (int i = threadIdx.x; i < E; i += blockDim.x) {
+      lo = fminf(lo, wc[i]);
+      hi = fmaxf(hi, wc[i]);
+    }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if ((threadIdx.x & 63) == 0) {
+      s_mm[0][threadIdx.x >> 6] = lo;
+      s_mm[1][threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    mn = fminf(fminf(s_mm[0][0], s_mm[0][1]), fminf(s_mm[0][2], s_mm[0][3]));
+    mx = fmaxf(fmaxf(s_mm[1][0], s_mm[1][1]), fmaxf(s_mm[1][2], s_mm[1][3]));
+  }
+  float s = (mx - mn) / qmax;  // quantize.py:71 (tensor, fp32)
+  s = fmaxf(s, 1e-8f);         // :73
+  const float neg_min = -mn;
+  if (threadIdx.x == 0) {
+    s_w[c] = s;
+    b_w[c] = (float)(128.0 * (double)s + (double)mn);
+    if (w_min_out) w_min_out[c] = mn;
+    if (w_max_out) w_max_out[c] = mx;
+  }
+  // packed row: [tap][cin_pad] codes, zero tail up to kpad
+  for (int i = threadIdx.x; i < kpad; i += blockDim.x) {
+    int8_t code = 0;
+    int tap = i / cin_pad;
+    int ci = i - tap * cin_pad;
+    if (tap < taps && ci < cin_g) {
+      float q = quant_code(wc[ci * taps + tap], neg_min, s, qmax);
+      code = (int8_t)((int)q - 128);
+    }
+    row[i] = code;
+  }
+  if (w_hat) {
+    for (int e = threadIdx.x; e < E; e += blockDim.x)
+      w_hat[(int64_t)c * E + e] = fake_quant(wc[e], neg_min, mn, s, qmax);
+  }
+  if (tap_sum) {
+    for (int tap = 0; tap < taps; ++tap) {
+      double acc = 0.0;
+      for (int ci = threadIdx.x; ci < cin_g; ci += blockDim.x)
+        acc += (double)fake_quant(wc[ci * taps + tap], neg_min, mn, s, qmax);
+      acc = wave_sum(acc);
+      __syncthreads();
+      if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) tap_sum[(int64_t)c * taps + tap] = (float)(s_red[0] + s_red[1] + s_red[2] + s_red[3]);
+    }
+  }
+}
+
+__global__ void border_table_kernel(const float* __restrict__ tap_sum, int cout, int kh, int kw,
+                                    const int* __restrict__ hrange, int nhc, const int* __restrict__ wrange,
+                                    int nwc, float b_x, float* __restrict__ table) {
+  int64_t total = (int64_t)nhc * nwc * cout;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % cout);
+    int cls = (int)(i / cout);
+    int wc = cls % nwc, hc = cls / nwc;
+    double acc = 0.0;
+    for (int r = hrange[2 * hc]; r < hrange[2 * hc + 1]; ++r)
+      for (int s = wrange[2 * wc]; s < wrange[2 * wc + 1]; ++s) acc += (double)tap_sum[(int64_t)c * kh * kw + r * kw + s];
+    table[i] = (float)((double)b_x * acc);
+  }
+}
+
+// ------------------------------------------------------------------ RangeBN eval
+__device__ __forceinline__ float rangebn_one(float x, float neg_min, float min, float scale, float qmax, float mu,
+                                             float sq, float wq, float bq) {
+  float xh = fake_quant(x, neg_min, min, scale, qmax);  // quantize_input  :462
+  float o = xh - mu;                                     // x - mean        :488
+  o = o * sq;                                            // * q(scale)      :488-489
+  o = o * wq;                                            // * q(weight)     :495
+  return o + bq;                                         // + q(bias)       :499
+}
+
+__global__ void rangebn_kernel(const float* __restrict__ x, float* y, int64_t total, int c, int hw, float neg_min,
+                               float min, float scale, float qmax, const float* __restrict__ mean,
+                               const float* __restrict__ sq, const float* __restrict__ wq,
+                               const float* __restrict__ bq, const float* residual, int relu) {
+  const bool vec = (hw & 3) == 0;
+  int64_t step = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < total; i += step) {
+    if (vec) {
+      int ch = (int)((i / hw) % c);
+      float mu = mean[ch], a = sq[ch], b = wq[ch], d = bq[ch];
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      float4 o;
+      o.x = rangebn_one(v.x, neg_min, min, scale, qmax, mu, a, b, d);
+      o.y = rangebn_one(v.y, neg_min, min, scale, qmax, mu, a, b, d);
+      o.z = rangebn_one(v.z, neg_min, min, scale, qmax, mu, a, b, d);
+      o.w = rangebn_one(v.w, neg_min, min, scale, qmax, mu, a, b, d);
+      if (residual) {
+        float4 r = *reinterpret_cast<const float4*>(residual + i);
+        o.x = o.x + r.x; o.y = o.y + r.y; o.z = o.z + r.z; o.w = o.w + r.w;
+      }
+      if (relu) {
+        o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+      }
+      *reinterpret_cast<float4*>(y + i) = o;
+    } else {
+      for (int64_t j = i; j < total && j < i + 4; ++j) {
+        int ch = (int)((j / hw) % c);
+        float o = rangebn_one(x[j], neg_min, min, scale, qmax, mean[ch], sq[ch], wq[ch], bq[ch]);
+        if (residual) o = o + residual[j];
+        if (relu) o = fmaxf(o, 0.f);
+        y[j] = o;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ depthwise
+__global__ void dwconv_kernel(const float* __restrict__ x, int n, int c, int h, int w,
+                              const float* __restrict__ w_hat, int kh, int kw, int sh, int sw, int ph, int pw,
+                              int ho, int wo, float neg_min, float min, float scale, float qmax,
+                              const float* __restrict__ bias, float* __restrict__ y) {
+  int64_t total = (int64_t)n * c * ho * wo;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int ox = (int)(i % wo);
+    int64_t t = i / wo;
+    int oy = (int)(t % ho);
+    int64_t nc = t / ho;
+    int ch = (int)(nc % c);
+    const float* xp = x + nc * h * w;
+    const float* wp = w_hat + (int64_t)ch * kh * kw;
+    float acc = 0.f;
+    for (int r = 0; r < kh; ++r) {
+      int iy = oy * sh - ph + r;
+      if (iy < 0 || iy >= h) continue;
+      for (int s = 0; s < kw; ++s) {
+        int ix = ox * sw - pw + s;
+        if (ix < 0 || ix >= w) continue;
+        float xh = fake_quant(xp[iy * w + ix], neg_min, min, scale, qmax);
+        acc = fmaf(xh, wp[r * kw + s], acc);
+      }
+    }
+    if (bias) acc = acc + bias[ch];
+    y[i] = acc;
+  }
+}
+
+static int grid_for(int64_t work, int block) {
+  int64_t g = cdiv(work, block);
+  if (g > 256 * 32) g = 256 * 32;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace qnn
+
+using namespace qnn;
+
+extern "C" {
+
+int qnn_abi_version(void) { return QNN_ABI_VERSION; }
+
+const char* qnn_last_error(void) { return qnn::g_last_error.c_str(); }
+
+int qnn_fake_quant_f32(const float* x, float* y, int64_t n, float neg_min, float min, float scale, float qmax,
+                       qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0, "n < 0");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(x && y, "null pointer");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  hipLaunchKernelGGL(fake_quant_kernel, dim3(grid_for(cdiv(n, 4), 256)), dim3(256), 0, (hipStream_t)stream, x, y,
+                     n, neg_min, min, scale, qmax);
+  QNN_LAUNCH_CHECK("qnn_fake_quant_f32");
+  return QNN_OK;
+}
+
+int qnn_fake_quant_rows_f32(const float* x, float* y, int rows, int64_t cols, const float* mins, const float* maxs,
+                            float qmax, qnn_stream_t stream) {
+  QNN_REQUIRE(rows >= 0 && cols >= 0 && rows <= 65535, "bad shape (rows must be <= 65535)");
+  if (rows == 0 || cols == 0) return QNN_OK;
+  QNN_REQUIRE(x && y && mins && maxs, "null pointer");
+  int gx = (int)cdiv(cols, 256);
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(fake_quant_rows_kernel, dim3(gx, rows), dim3(256), 0, (hipStream_t)stream, x, y, rows, cols, mins,
+                     maxs, qmax);
+  QNN_LAUNCH_CHECK("qnn_fake_quant_rows_f32");
+  return QNN_OK;
+}
+
+int qnn_fake_quant_vec_f32(const float* x, float* y, int n, float qmax, int scale_mode, float* range_out,
+                           qnn_stream_t stream) {
+  QNN_REQUIRE(n > 0 && n <= 65536, "n must be in [1, 65536]");
+  QNN_REQUIRE(x && y, "null pointer");
+  QNN_REQUIRE(scale_mode == 0 || scale_mode == 1, "scale_mode must be 0 or 1");
+  hipLaunchKernelGGL(fake_quant_vec_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, y, n, qmax, scale_mode,
+                     range_out);
+  QNN_LAUNCH_CHECK("qnn_fake_quant_vec_f32");
+  return QNN_OK;
+}
+
+int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, int w, int cp, float neg_min,
+                               float scale, float qmax, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && c > 0 && h > 0 && w > 0, "bad shape");
+  QNN_REQUIRE(cp >= c && cp % 16 == 0, "cp must be a multiple of 16 and >= c");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(x && q, "null pointer");
+  int64_t work = (int64_t)n * h * w * (cp / 16);
+  hipLaunchKernelGGL(quantize_nchw_nhwc8_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream, x, q,
+                     n, c, h * w, cp, neg_min, scale, qmax);
+  QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_nhwc8");
+  return QNN_OK;
+}
+
+int qnn_pack_weight_i8(const float* w, int cout, int cin_g, int kh, int kw, int cin_pad, int cout_pad, float qmax,
+                       const float* w_min_in, const float* w_max_in, int8_t* wq, float* s_w, float* b_w,
+                       float* tap_sum, float* w_hat, float* w_min_out, float* w_max_out, qnn_stream_t stream) {
+  QNN_REQUIRE(cout > 0 && cin_g > 0 && kh > 0 && kw > 0, "bad shape");
+  QNN_REQUIRE(cin_pad >= cin_g && cout_pad >= cout, "padding smaller than shape");
+  QNN_REQUIRE(w && wq && s_w && b_w, "null pointer");
+  QNN_REQUIRE((w_min_in == nullptr) == (w_max_in == nullptr), "w_min_in/w_max_in must both be set or both null");
+  int kpad = (int)(cdiv((int64_t)kh * kw * cin_pad, 64) * 64);
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(cout_pad), dim3(256), 0, (hipStream_t)stream, w, cout, cin_g, kh, kw,
+                     cin_pad, kpad, qmax, w_min_in, w_max_in, wq, s_w, b_w, tap_sum, w_hat, w_min_out, w_max_out);
+  QNN_LAUNCH_CHECK("qnn_pack_weight_i8");
+  return QNN_OK;
+}
+
+int qnn_conv_border_table(const float* tap_sum, int cout, int kh, int kw, const int* hrange, int nhc,
+                          const int* wrange, int nwc, float b_x, float* table, qnn_stream_t stream) {
+  QNN_REQUIRE(cout > 0 && kh > 0 && kw > 0 && nhc > 0 && nwc > 0, "bad shape");
+  QNN_REQUIRE(tap_sum && hrange && wrange && table, "null pointer");
+  int64_t work = (int64_t)nhc * nwc * cout;
+  hipLaunchKernelGGL(border_table_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream, tap_sum, cout,
+                     kh, kw, hrange, nhc, wrange, nwc, b_x, table);
+  QNN_LAUNCH_CHECK("qnn_conv_border_table");
+  return QNN_OK;
+}
+
+int qnn_rangebn_f32(const float* x, float* y, int n, int c, int hw, float neg_min, float min, float scale, float qmax,
+                    const float* mean, const float* sq, const float* wq, const float* bq, const float* residual,
+                    int relu, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && c > 0 && hw > 0, "bad shape");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(x && y && mean && sq && wq && bq, "null pointer");
+  int64_t total = (int64_t)n * c * hw;
+  if ((hw & 3) == 0) {
+    QNN_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && (!residual || ((uintptr_t)residual & 15) == 0),
+                "x/y/residual must be 16-byte aligned");
+  }
+  hipLaunchKernelGGL(rangebn_kernel, dim3(grid_for(cdiv(total, 4), 256)), dim3(256), 0, (hipStream_t)stream, x, y,
+                     total, c, hw, neg_min, min, scale, qmax, mean, sq, wq, bq, residual, relu);
+  QNN_LAUNCH_CHECK("qnn_rangebn_f32");
+  return QNN_OK;
+}
+
+int qnn_dwconv2d_fwd(const float* x, int n, int c, int h, int w, const float* w_hat, int kh, int kw, int sh, int sw,
+                     int ph, int pw, int ho, int wo, float neg_min, float min, float scale, float qmax,
+                     const float* bias, float* y, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && c > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && sh > 0 && sw > 0, "bad shape");
+  QNN_REQUIRE(ho == (h + 2 * ph - kh) / sh + 1 && wo == (w + 2 * pw - kw) / sw + 1, "ho/wo inconsistent");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(x && w_hat && y, "null pointer");
+  int64_t total = (int64_t)n * c * ho * wo;
+  hipLaunchKernelGGL(dwconv_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, x, n, c, h, w,
+                     w_hat, kh, kw, sh, sw, ph, pw, ho, wo, neg_min, min, scale, qmax, bias, y);
+  QNN_LAUNCH_CHECK("qnn_dwconv2d_fwd");
+  return QNN_OK;
+}
+
+}  // extern "C"

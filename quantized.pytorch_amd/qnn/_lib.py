@@ -1,0 +1,94 @@
+"""ctypes binding of libqnn_hip.so (the C ABI declared in include/qnn.h).
+
+The library is built in-tree (`make -C quantized.pytorch_amd`) and loaded from
+this directory only.  There is no fallback: if it is missing, every quantized
+op on a ROCm device raises `QnnLibraryError`.
+
+torch must be imported before the library is loaded so that its HIP runtime
+(SONAME libamdhip64.so.7) is the one the library binds to; streams and device
+pointers are then shared with PyTorch.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (binds the process HIP runtime first)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqnn_hip.so")
+
+ABI_VERSION = 1
+
+c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+# name -> argtypes (restype is int status for all but the two metadata calls)
+SIGNATURES = {
+    "qnn_fake_quant_f32": [c_ptr, c_ptr, c_i64, c_float, c_float, c_float, c_float, c_ptr],
+    "qnn_fake_quant_rows_f32": [c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_float, c_ptr],
+    "qnn_fake_quant_vec_f32": [c_ptr, c_ptr, c_int, c_float, c_int, c_ptr, c_ptr],
+    "qnn_quantize_nchw_to_nhwc8": [c_ptr, c_ptr, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_ptr],
+    "qnn_pack_weight_i8": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_ptr, c_ptr, c_ptr, c_ptr,
+                           c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "qnn_conv_border_table": [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_float, c_ptr, c_ptr],
+    "qnn_qconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_int, c_ptr],
+    "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
+    "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,
+                        c_ptr, c_ptr, c_int, c_ptr],
+}
+
+
+class QnnLibraryError(RuntimeError):
+    pass
+
+
+class QnnError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load and type the library (cached).  Raises QnnLibraryError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise QnnLibraryError(
+            f"qnn: {path} not found - build it with `make -C quantized.pytorch_amd` "
+            "(the int8 MI355X path has no fallback)")
+    lib = ctypes.CDLL(path)
+    lib.qnn_abi_version.restype = c_int
+    lib.qnn_abi_version.argtypes = []
+    lib.qnn_last_error.restype = ctypes.c_char_p
+    lib.qnn_last_error.argtypes = []
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = c_int
+    v = lib.qnn_abi_version()
+    if v != ABI_VERSION:
+        raise QnnLibraryError(f"qnn: ABI version mismatch (library {v}, bindings {ABI_VERSION})")
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point and raise QnnError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.qnn_last_error().decode(errors="replace")
+        raise QnnError(f"{name} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    """hipStream_t of the current PyTorch stream on t's device."""
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)

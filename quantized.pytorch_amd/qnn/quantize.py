@@ -1,0 +1,714 @@
+"""Drop-in mirror of models/modules/quantize.py for MI355X (ROCm / gfx950).
+
+Same public surface as the reference: `quantize`,
+`quantize_grad`, `QuantNode`, `QuantMeasure`, `QConv2d`, `QLinear`, `RangeBN`,
+the tree helpers (`set_measure_mode`, `set_quant_mode`, `overwrite_params`,
+`freeze_quant_params`, `set_global_quantization_method`, ...), identical
+constructor arguments, buffers and state_dict keys, so reference checkpoints
+`load_state_dict(strict=True)` and models/resnet_quantized.py /
+models/mobilenet_quantized.py run unchanged on these classes.
+
+Execution model:
+* quantized forward (enable_quant, eval or train) on a ROCm device -> the HIP
+  C ABI (`include/qnn.h`): int8 MFMA implicit-GEMM conv / GEMM, fp32 epilogue.
+  There is no fallback: a missing library raises `QnnLibraryError`, and a CPU
+  tensor raises `RuntimeError` (the reference's CPU fake-quant forward is the
+  oracle under oracle/, not part of this package).
+* measure mode (enable_quant=False) keeps the reference semantics: float conv /
+  linear (`F.conv2d`/`F.linear`, quantize.py:350-352, :429-430) and the
+  QuantMeasure / RangeBN statistics updates (:225-239, :466-482) in torch ops.
+  This is calibration, off the hot path.
+* forward only: no autograd through the int8 path (training is out of scope,
+  SURVEY.md §2 row 1).
+
+Host-scalar caching: the reference reads `float(running_min)` on every call
+(2 device->host syncs per layer, quantize.py:249).  Here ranges, packed weights
+and epilogue vectors are cached and keyed on the tensors' version counters, so a
+steady-state eval forward issues no synchronisation.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+_QMEASURE_ALPHA = {2: 2.83, 3: 3.89, 4: 5.03, 5: 6.2, 6: 7.41, 7: 8.64, 8: 9.89}  # quantize.py:214
+
+
+def _qmax(num_bits):
+    if num_bits is None or num_bits < 1 or num_bits > 8:
+        raise ValueError(f"qnn: the int8 path supports 1..8-bit quantization, got num_bits={num_bits}")
+    return float(2 ** num_bits - 1)
+
+
+def _require_device(t, what):
+    if not t.is_cuda:
+        raise RuntimeError(f"qnn: {what} runs on the MI355X int8 path only (ROCm device tensor required, got "
+                           f"{t.device}); the reference's CPU fake-quant forward lives in oracle/ as a test checker")
+    if t.dtype != torch.float32:
+        raise TypeError(f"qnn: {what} expects float32 input, got {t.dtype}")
+
+
+def float_scale(mn, mx, num_bits):
+    """Scale of the Python-float path (quantize.py:71-75): double, floored at 1e-8.
+    The kernels receive its fp32 rounding (the cast PyTorch applies at div_/mul_)."""
+    return max((float(mx) - float(mn)) / (2.0 ** num_bits - 1.0), 1e-8)
+
+
+def _round_up(a, b):
+    return (a + b - 1) // b * b
+
+
+# ============================================================ functional quantize
+def quantize(x, num_bits=8, min_value=None, max_value=None, num_chunks=None, stochastic=False, inplace=False):
+    """quantize.py:159-160 with its effective binding: `stochastic` is never set and
+    the asymmetric branch always runs.  GPU only."""
+    _require_device(x, "quantize()")
+    qmax = _qmax(num_bits)
+    xc = x.contiguous()
+    out = xc if inplace else torch.empty_like(xc)
+    st = _lib.stream_of(xc)
+    if min_value is None or max_value is None:
+        if (min_value is None) != (max_value is None):
+            raise NotImplementedError("qnn: quantize() with only one of min/max given")
+        B = x.shape[0]
+        chunks = B if num_chunks is None else num_chunks
+        if max(B // chunks, 1) != 1 or xc.numel() > 65536:
+            raise NotImplementedError("qnn: per-chunk ranges are only used by training paths (out of scope)")
+        _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(xc), _lib.ptr(out), xc.numel(), qmax, 0, None, st)
+        return out
+    if torch.is_tensor(min_value) or torch.is_tensor(max_value):
+        mn = torch.as_tensor(min_value, dtype=torch.float32, device=x.device)
+        mx = torch.as_tensor(max_value, dtype=torch.float32, device=x.device)
+        rows = mn.numel()
+        if rows == 1:
+            mn, mx = mn.reshape(1), mx.reshape(1)
+        elif mn.shape[0] != x.shape[0] or mn.numel() != x.shape[0]:
+            raise NotImplementedError("qnn: tensor ranges must be per-tensor or per-dim-0")
+        mn, mx = mn.contiguous(), mx.contiguous()
+        _lib.call("qnn_fake_quant_rows_f32", _lib.ptr(xc), _lib.ptr(out), rows, xc.numel() // rows,
+                  _lib.ptr(mn), _lib.ptr(mx), qmax, st)
+        return out
+    s = float_scale(min_value, max_value, num_bits)
+    _lib.call("qnn_fake_quant_f32", _lib.ptr(xc), _lib.ptr(out), xc.numel(), -float(min_value), float(min_value),
+              s, qmax, st)
+    return out
+
+
+def quantize_grad(x, num_bits=8, min_value=None, max_value=None, stochastic=True, inplace=False):
+    """UniformQuantizeGrad (quantize.py:112-121, :163-164): identity in forward."""
+    return x
+
+
+def conv2d_biprec(input, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, num_bits_grad=None):
+    """quantize.py:142-148.  The forward value out1 + out2 - out1 equals one conv
+    bitwise; kept for API completeness (float operands)."""
+    return F.conv2d(input, weight, bias, stride, padding, dilation, groups)
+
+
+def linear_biprec(input, weight, bias=None, num_bits_grad=None):
+    """quantize.py:151-156 (forward value == one linear)."""
+    return F.linear(input, weight, bias)
+
+
+# ============================================================ QuantNode / QuantMeasure
+class QuantNode:
+    """quantize.py:177-196."""
+
+    def __init__(self):
+        self.enable_quant = True
+        self.freeze_param_dyn_range = False
+
+    def set_measure_mode(self, measure, momentum=None):
+        self.enable_quant = not measure
+        if momentum and isinstance(self, QuantMeasure):
+            self.momentum = momentum
+        else:
+            if isinstance(self, nn.Module):
+                for q in self._modules.values():
+                    if isinstance(q, QuantNode):
+                        q.set_measure_mode(measure, momentum=momentum)
+
+    def overwrite_params(self, logging=None):
+        if isinstance(self, nn.Module):
+            for q in self._modules.values():
+                if isinstance(q, QuantNode):
+                    q.overwrite_params(logging)
+
+
+class QuantMeasure(nn.Module, QuantNode):
+    """quantize.py:198-268: per-tensor activation range; eval = running range."""
+    _QMEASURE_SUPPORTED_METHODS = ["avg", "aciq"]
+
+    def __init__(self, num_bits=8, momentum=None, method="avg"):
+        super().__init__()
+        QuantNode.__init__(self)
+        assert method in QuantMeasure._QMEASURE_SUPPORTED_METHODS
+        self.register_buffer("running_min", torch.zeros(1))
+        self.register_buffer("running_max", torch.zeros(1))
+        self.register_buffer("num_measurements", torch.zeros(1))
+        self.register_buffer("running_var", torch.ones(1))
+        self.register_buffer("running_mean", torch.zeros(1))
+        self.momentum = momentum
+        self.num_bits = num_bits
+        self.method = method
+        self.laplace_alpha = _QMEASURE_ALPHA.get(num_bits)
+        self._range_cache = None
+
+    def _momentum_update_stat(self, new_value, running_stat, momentum=None):
+        momentum = momentum or self.momentum or self.num_measurements / (self.num_measurements + 1)
+        running_stat.mul_(momentum).add_(new_value * (1 - momentum))
+
+    def _observe(self, input_):
+        """Train-branch statistics (quantize.py:225-239); returns the batch range."""
+        min_value = input_.view(input_.size(0), -1).min(-1)[0].mean()
+        self._momentum_update_stat(min_value, self.running_min)
+        max_value = input_.view(input_.size(0), -1).max(-1)[0].mean()
+        self._momentum_update_stat(max_value, self.running_max)
+        mean = input_.mean()
+        std = input_.std(unbiased=True)
+        self._momentum_update_stat(mean, self.running_mean)
+        self._momentum_update_stat(std, self.running_var)
+        self.num_measurements += 1
+        if self.method == "aciq":
+            min_value, max_value = self._get_aciq_range(std, mean, min_value, max_value)
+        return float(min_value), float(max_value)
+
+    def _eval_range(self):
+        """(float min, float max) of the eval branch (:241-249), cached on buffer versions."""
+        if self.method == "aciq":
+            # `std += 1e-8` mutates running_var in place every call (:258): keep that.
+            lo, hi = self._get_aciq_range(self.running_var, self.running_mean, self.running_min, self.running_max)
+            return float(lo), float(hi)
+        key = (self.running_min.data_ptr(), self.running_min._version,
+               self.running_max.data_ptr(), self.running_max._version)
+        if self._range_cache is None or self._range_cache[0] != key:
+            self._range_cache = (key, (float(self.running_min), float(self.running_max)))
+        return self._range_cache[1]
+
+    def range_for(self, input):
+        """The (min, max) the forward quantizes `input` with, applying the
+        training-branch side effects exactly when the reference does."""
+        if self.training:
+            with torch.no_grad():
+                return self._observe(input.detach())
+        return self._eval_range()
+
+    def forward(self, input):
+        rng = self.range_for(input)
+        if self.enable_quant:
+            return quantize(input, self.num_bits, min_value=rng[0], max_value=rng[1])
+        return input
+
+    def _get_measured_range(self):
+        return float(self.running_min), float(self.running_max)
+
+    def _get_aciq_range(self, std, mean, tmin, tmax):
+        with torch.no_grad():
+            std += 1e-8
+            assert self.laplace_alpha, "aciq not supported for module num bits"
+            clip_val = std * self.laplace_alpha
+            assert clip_val > 0, "invalid clip value!"
+            max_range = tmax - tmin
+            clip_val = min(max_range / 2, clip_val)
+            min_value = max(tmin, mean - clip_val)
+            max_value = min(tmax, mean + clip_val)
+        return min_value, max_value
+
+
+# ============================================================ packed operands
+class _Packed:
+    """Device-resident int8 operands of one QConv2d/QLinear weight version."""
+    __slots__ = ("key", "wq", "s_w", "b_w", "tap_sum", "w_hat", "qbias", "cin_pad", "cout_pad", "geom", "epi")
+
+
+def _border_classes(size, k, stride, pad, out):
+    """Distinct [lo, hi) valid-tap ranges over output positions (zero padding)."""
+    cls, ranges, ids = [], [], {}
+    for o in range(out):
+        lo = max(0, pad - o * stride)
+        hi = min(k, size + pad - o * stride)
+        key = (lo, hi)
+        if key not in ids:
+            ids[key] = len(ranges)
+            ranges.append(key)
+        cls.append(ids[key])
+    return cls, ranges
+
+
+class _QLayerMixin:
+    """Shared int8 machinery of QConv2d / QLinear (QuantNode subclasses)."""
+
+    def _init_qcache(self):
+        self._qpack = None
+
+    def _weight4(self):
+        w = self.weight
+        return w if w.dim() == 4 else w.view(w.shape[0], w.shape[1], 1, 1)
+
+    def _pack(self, depthwise=False):
+        w = self.weight
+        bias = self.bias
+        freeze = bool(self.freeze_param_dyn_range)
+        key = (w.data_ptr(), w._version, None if bias is None else (bias.data_ptr(), bias._version), freeze,
+               self.num_bits_weight, self.bias_quant, depthwise, w.device)
+        pk = self._qpack
+        if pk is not None and pk.key == key:
+            return pk
+        if not self.per_channel:
+            # the reference assigns a float to a registered buffer here and raises (quantize.py:325-326)
+            raise TypeError("cannot assign 'float' as buffer 'weight_min' (torch.Tensor or None expected)")
+        _require_device(w, type(self).__name__)
+        qmax = _qmax(self.num_bits_weight)
+        w4 = self._weight4().detach().contiguous()
+        cout, cin_g, kh, kw = w4.shape
+        dev = w.device
+        pk = _Packed()
+        pk.key = key
+        pk.cin_pad = _round_up(cin_g, 16)
+        pk.cout_pad = _round_up(cout, 64) if cout <= 64 else _round_up(cout, 128)
+        kpad = _round_up(kh * kw * pk.cin_pad, 64)
+        pk.wq = torch.empty((pk.cout_pad, kpad), dtype=torch.int8, device=dev)
+        pk.s_w = torch.empty(cout, dtype=torch.float32, device=dev)
+        pk.b_w = torch.empty(cout, dtype=torch.float32, device=dev)
+        pk.tap_sum = torch.empty((cout, kh * kw), dtype=torch.float32, device=dev)
+        pk.w_hat = torch.empty((cout, cin_g * kh * kw), dtype=torch.float32, device=dev) if depthwise else None
+        st = _lib.stream_of(w4)
+        if freeze:
+            wmin_in = self.weight_min.detach().reshape(-1).float().contiguous()
+            wmax_in = self.weight_max.detach().reshape(-1).float().contiguous()
+            wmin_out = wmax_out = None
+        else:
+            wmin_in = wmax_in = None
+            # weight_min/max buffers are rewritten every forward (quantize.py:317-323)
+            wmin_out = torch.empty(cout, dtype=torch.float32, device=dev)
+            wmax_out = torch.empty(cout, dtype=torch.float32, device=dev)
+        _lib.call("qnn_pack_weight_i8", _lib.ptr(w4), cout, cin_g, kh, kw, pk.cin_pad, pk.cout_pad, qmax,
+                  _lib.ptr(wmin_in), _lib.ptr(wmax_in), _lib.ptr(pk.wq), _lib.ptr(pk.s_w), _lib.ptr(pk.b_w),
+                  _lib.ptr(pk.tap_sum), _lib.ptr(pk.w_hat), _lib.ptr(wmin_out), _lib.ptr(wmax_out), st)
+        if not freeze:
+            self.weight_min = wmin_out.view(self.scale_shape)
+            self.weight_max = wmax_out.view(self.scale_shape)
+        pk.qbias = None
+        if bias is not None:
+            b = bias.detach().contiguous()
+            rng = torch.empty(2, dtype=torch.float32, device=dev)
+            if self.bias_quant:
+                pk.qbias = torch.empty_like(b)
+                _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(b), _lib.ptr(pk.qbias), b.numel(), qmax, 0,
+                          _lib.ptr(rng), st)
+            else:
+                pk.qbias = b
+                tmp = torch.empty_like(b)
+                _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(b), _lib.ptr(tmp), b.numel(), qmax, 0, _lib.ptr(rng), st)
+            if not freeze:
+                # quantize.py:328-330 (tensor assignment, also when bias_quant is off)
+                self.bias_min = rng[0]
+                self.bias_max = rng[1]
+        pk.geom = {}
+        pk.epi = {}
+        self._qpack = pk
+        return pk
+
+    def _geometry(self, pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev):
+        gk = (H, W)
+        g = pk.geom.get(gk)
+        if g is None:
+            hc, hr = _border_classes(H, kh, sh, ph, Ho)
+            wc, wr = _border_classes(W, kw, sw, pw, Wo)
+            t = lambda a: torch.tensor(np.asarray(a, dtype=np.int32).reshape(-1), device=dev)
+            g = (t(hc), t(hr), len(hr), t(wc), t(wr), len(wr))
+            pk.geom[gk] = g
+        return g
+
+    def _epilogue(self, pk, g, gk, s_x, b_x, kh, kw):
+        ek = (gk, s_x, b_x)
+        e = pk.epi.get(ek)
+        if e is None:
+            hcls, hr, nhc, wcls, wr, nwc = g
+            cout = pk.s_w.numel()
+            sxsw = (pk.s_w.double() * float(s_x)).float()
+            sxbw = (pk.b_w.double() * float(s_x)).float()
+            table = torch.empty((nhc, nwc, cout), dtype=torch.float32, device=pk.s_w.device)
+            _lib.call("qnn_conv_border_table", _lib.ptr(pk.tap_sum), cout, kh, kw, _lib.ptr(hr), nhc, _lib.ptr(wr),
+                      nwc, float(b_x), _lib.ptr(table), _lib.stream_of(table))
+            e = (sxsw, sxbw, table)
+            if len(pk.epi) > 8:
+                pk.epi.clear()
+            pk.epi[ek] = e
+        return e
+
+    def _int8_forward(self, x4, rng, stride, padding, out_layout=0):
+        """Quantize x (NCHW fp32) to NHWC8 codes and run the MFMA conv."""
+        pk = self._pack()
+        w4 = self._weight4()
+        cout, cin_g, kh, kw = w4.shape
+        N, C, H, W = x4.shape
+        if C != cin_g:
+            raise RuntimeError(f"qnn: expected {cin_g} input channels, got {C}")
+        sh, sw = stride
+        ph, pw = padding
+        Ho = (H + 2 * ph - kh) // sh + 1
+        Wo = (W + 2 * pw - kw) // sw + 1
+        if Ho <= 0 or Wo <= 0:
+            raise RuntimeError("qnn: output size is empty")
+        qmax = _qmax(self.num_bits)
+        mn, mx = rng
+        s = float_scale(mn, mx, self.num_bits)
+        s32 = float(np.float32(s))
+        b_x = 128.0 * s32 + float(np.float32(mn))
+        dev = x4.device
+        st = _lib.stream_of(x4)
+        xq = torch.empty((N, H, W, pk.cin_pad), dtype=torch.int8, device=dev)
+        _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, pk.cin_pad, -float(mn), s,
+                  qmax, st)
+        g = self._geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev)
+        sxsw, sxbw, table = self._epilogue(pk, g, (H, W), s32, b_x, kh, kw)
+        if out_layout == 0:
+            y = torch.empty((N, cout, Ho, Wo), dtype=torch.float32, device=dev)
+        else:
+            y = torch.empty((N, Ho, Wo, cout), dtype=torch.float32, device=dev)
+        _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), N, H, W, pk.cin_pad, _lib.ptr(pk.wq), cout, pk.cout_pad, kh, kw,
+                  sh, sw, ph, pw, Ho, Wo, _lib.ptr(sxsw), _lib.ptr(sxbw), _lib.ptr(table), _lib.ptr(g[0]), _lib.ptr(g[3]),
+                  g[5], _lib.ptr(pk.qbias), _lib.ptr(y), out_layout, st)
+        return y
+
+
+# ============================================================ QConv2d
+class QConv2d(nn.Conv2d, QuantNode, _QLayerMixin):
+    """quantize.py:271-354."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, groups=1, bias=True,
+                 num_bits=8, num_bits_weight=None, num_bits_grad=None, biprecision=False, bias_quant=True,
+                 per_channel=True, **kwargs):
+        super().__init__(in_channels, out_channels, kernel_size, stride, padding, dilation, groups, bias, **kwargs)
+        QuantNode.__init__(self)
+        self._init_qcache()
+        self.num_bits = num_bits
+        self.num_bits_weight = num_bits_weight or num_bits
+        self.num_bits_grad = num_bits_grad
+        self.quantize_input = QuantMeasure(self.num_bits)
+        self.biprecision = biprecision
+        self.bias_quant = bias_quant and bias
+        self.per_channel = per_channel
+        if self.per_channel:
+            n_channels = self.weight.size(0)
+            dim = self.weight.dim()
+            self.scale_shape = (n_channels,) + (1,) * (dim - 1)
+            self.register_buffer("weight_min", self.weight.flatten(1).min(-1)[0].view(self.scale_shape))
+            self.register_buffer("weight_max", self.weight.flatten(1).max(-1)[0].view(self.scale_shape))
+        else:
+            self.register_buffer("weight_min", self.weight.min())
+            self.register_buffer("weight_max", self.weight.max())
+        if self.bias_quant:
+            self.register_buffer("bias_min", self.bias.min())
+            self.register_buffer("bias_max", self.bias.max())
+
+    def overwrite_params(self, logging=None):
+        """quantize.py:301-312: bake the fake-quantized weight (and bias) into the state_dict."""
+        sd = self.state_dict()
+        if logging:
+            logging.debug(f"quantizing parameters for {super().__str__()}")
+        with torch.no_grad():
+            sd.update({"weight": quantize(self.weight, num_bits=self.num_bits_weight, min_value=self.weight_min,
+                                          max_value=self.weight_max)})
+            if self.bias_quant:
+                sd.update({"bias": quantize(self.bias, min_value=self.bias_min, max_value=self.bias_max,
+                                            num_bits=self.num_bits_weight)})
+        self.load_state_dict(sd)
+
+    def _is_depthwise(self):
+        return self.groups > 1 and self.groups == self.in_channels == self.out_channels
+
+    def forward(self, input):
+        rng = self.quantize_input.range_for(input)
+        if not self.enable_quant:
+            return F.conv2d(input, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+        _require_device(input, "QConv2d")
+        if tuple(self.dilation) != (1, 1):
+            raise NotImplementedError("qnn: dilation != 1 is not on the int8 path")
+        if self.padding_mode != "zeros" or isinstance(self.padding, str):
+            raise NotImplementedError("qnn: only explicit zero padding is on the int8 path")
+        x = input.detach().contiguous()
+        with torch.no_grad():
+            if self._is_depthwise():
+                return self._dw_forward(x, rng)
+            if self.groups != 1:
+                raise NotImplementedError("qnn: grouped conv other than depthwise is not on the int8 path")
+            return self._int8_forward(x, rng, self.stride, self.padding)
+
+    def _dw_forward(self, x, rng):
+        pk = self._pack(depthwise=True)
+        N, C, H, W = x.shape
+        kh, kw = self.kernel_size
+        sh, sw = self.stride
+        ph, pw = self.padding
+        Ho = (H + 2 * ph - kh) // sh + 1
+        Wo = (W + 2 * pw - kw) // sw + 1
+        mn, mx = rng
+        s = float_scale(mn, mx, self.num_bits)
+        y = torch.empty((N, C, Ho, Wo), dtype=torch.float32, device=x.device)
+        _lib.call("qnn_dwconv2d_fwd", _lib.ptr(x), N, C, H, W, _lib.ptr(pk.w_hat), kh, kw, sh, sw, ph, pw, Ho, Wo,
+                  -float(mn), float(mn), s, _qmax(self.num_bits), _lib.ptr(pk.qbias), _lib.ptr(y), _lib.stream_of(x))
+        return y
+
+
+# ============================================================ QLinear
+class QLinear(nn.Linear, QuantNode, _QLayerMixin):
+    """quantize.py:357-432."""
+
+    def __init__(self, in_features, out_features, bias=True, num_bits=8, num_bits_weight=None, num_bits_grad=None,
+                 biprecision=False, bias_quant=True, per_channel=True, **kwargs):
+        super().__init__(in_features, out_features, bias, **kwargs)
+        QuantNode.__init__(self)
+        self._init_qcache()
+        self.num_bits = num_bits
+        self.num_bits_weight = num_bits_weight or num_bits
+        self.num_bits_grad = num_bits_grad
+        self.biprecision = biprecision
+        self.quantize_input = QuantMeasure(self.num_bits)
+        self.bias_quant = bias_quant and bias
+        self.per_channel = per_channel
+        if self.per_channel:
+            n_channels = self.weight.size(0)
+            dim = self.weight.dim()
+            self.scale_shape = (n_channels,) + (1,) * (dim - 1)
+            self.register_buffer("weight_min", self.weight.flatten(1).min(-1)[0].view(self.scale_shape))
+            self.register_buffer("weight_max", self.weight.flatten(1).max(-1)[0].view(self.scale_shape))
+        else:
+            self.register_buffer("weight_min", self.weight.min())
+            self.register_buffer("weight_max", self.weight.max())
+        if self.bias_quant:
+            self.register_buffer("bias_min", self.bias.min())
+            self.register_buffer("bias_max", self.bias.max())
+
+    def overwrite_params(self, logging=None):
+        """quantize.py:386-396."""
+        sd = self.state_dict()
+        if logging:
+            logging.debug(f"quantizing parameters for {super().__str__()}")
+        with torch.no_grad():
+            sd.update({"weight": quantize(self.weight, num_bits=self.num_bits_weight, min_value=self.weight_min,
+                                          max_value=self.weight_max)})
+            if self.bias_quant:
+                sd.update({"bias": quantize(self.bias, min_value=self.bias_min, max_value=self.bias_max,
+                                            num_bits=self.num_bits_weight)})
+        self.load_state_dict(sd)
+
+    def forward(self, input):
+        rng = self.quantize_input.range_for(input)
+        if not self.enable_quant:
+            return F.linear(input, self.weight, self.bias)
+        _require_device(input, "QLinear")
+        lead = input.shape[:-1]
+        x = input.detach().reshape(-1, input.shape[-1]).contiguous()
+        with torch.no_grad():
+            y = self._int8_forward(x.view(x.shape[0], x.shape[1], 1, 1), rng, (1, 1), (0, 0))
+        return y.view(*lead, self.out_features)
+
+
+# ============================================================ RangeBN
+class RangeBN(nn.Module):
+    """quantize.py:435-505 (normalized RangeBN).  Eval on a ROCm device runs one
+    fused HIP kernel; train (calibration) keeps the reference's torch-op statistics."""
+
+    def __init__(self, num_features, dim=1, momentum=0.1, affine=True, num_chunks=16, eps=1e-5, num_bits=8,
+                 num_bits_grad=8):
+        super().__init__()
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.zeros(num_features))
+        self.momentum = momentum
+        self.dim = dim
+        if affine:
+            self.bias = nn.Parameter(torch.Tensor(num_features))
+            self.weight = nn.Parameter(torch.Tensor(num_features))
+        else:
+            self.register_parameter("bias", None)
+            self.register_parameter("weight", None)
+        self.num_bits = num_bits
+        self.num_bits_grad = num_bits_grad
+        self.quantize_input = QuantMeasure(self.num_bits)
+        self.eps = eps
+        self.num_chunks = num_chunks
+        self._pcache = None
+        self.reset_params()
+
+    def reset_params(self):
+        if self.weight is not None:
+            self.weight.data.uniform_()
+        if self.bias is not None:
+            self.bias.data.zero_()
+
+    def _params(self, scale):
+        """Fake-quantized (scale, weight, bias) vectors (:486-499), cached on versions."""
+        w, b = self.weight, self.bias
+        key = (scale.data_ptr(), scale._version, None if w is None else (w.data_ptr(), w._version),
+               None if b is None else (b.data_ptr(), b._version), self.num_bits)
+        if self._pcache is not None and self._pcache[0] == key:
+            return self._pcache[1]
+        qmax = _qmax(self.num_bits)
+        st = _lib.stream_of(scale)
+        C = scale.numel()
+        sq = torch.empty(C, dtype=torch.float32, device=scale.device)
+        _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(scale.contiguous()), _lib.ptr(sq), C, qmax, 1, None, st)
+        if w is not None:
+            wq = torch.empty_like(sq)
+            _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(w.detach().contiguous()), _lib.ptr(wq), C, qmax, 1, None, st)
+        else:
+            wq = torch.ones_like(sq)
+        if b is not None:
+            bq = torch.empty_like(sq)
+            _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(b.detach().contiguous()), _lib.ptr(bq), C, qmax, 0, None, st)
+        else:
+            bq = torch.zeros_like(sq)
+        out = (sq, wq, bq)
+        self._pcache = (key, out)
+        return out
+
+    def forward(self, x):
+        if self.training or not self.quantize_input.enable_quant:
+            return self._forward_reference_ops(x)
+        _require_device(x, "RangeBN")
+        squeeze = x.dim() == 2
+        x4 = x.unsqueeze(-1).unsqueeze(-1) if squeeze else x
+        x4 = x4.detach().contiguous()
+        rng = self.quantize_input.range_for(x4)
+        mn, mx = rng
+        s = float_scale(mn, mx, self.num_bits)
+        N, C, H, W = x4.shape
+        with torch.no_grad():
+            sq, wq, bq = self._params(self.running_var)
+            y = torch.empty_like(x4)
+            _lib.call("qnn_rangebn_f32", _lib.ptr(x4), _lib.ptr(y), N, C, H * W, -float(mn), float(mn), s,
+                      _qmax(self.num_bits), _lib.ptr(self.running_mean), _lib.ptr(sq), _lib.ptr(wq), _lib.ptr(bq),
+                      None, 0, _lib.stream_of(x4))
+        if y.size(3) == 1 and y.size(2) == 1:
+            y = y.squeeze(-1).squeeze(-1)
+        return y
+
+    def _forward_reference_ops(self, x):
+        """Train / measure-mode branch with torch ops (quantize.py:461-505)."""
+        x = self.quantize_input(x)
+        if x.dim() == 2:
+            x = x.unsqueeze(-1).unsqueeze(-1)
+        if self.training:
+            B, C, H, W = x.shape
+            y = x.transpose(0, 1).contiguous()
+            y = y.view(C, self.num_chunks, B * H * W // self.num_chunks)
+            mean_max = y.max(-1)[0].mean(-1)
+            mean_min = y.min(-1)[0].mean(-1)
+            mean = y.view(C, -1).mean(-1)
+            scale_fix = (0.5 * 0.35) * (1 + (math.pi * math.log(4)) ** 0.5) / ((2 * math.log(y.size(-1))) ** 0.5)
+            scale = 1 / ((mean_max - mean_min) * scale_fix + self.eps)
+            self.running_mean.detach().mul_(self.momentum).add_(mean * (1 - self.momentum))
+            self.running_var.detach().mul_(self.momentum).add_(scale * (1 - self.momentum))
+        else:
+            mean = self.running_mean
+            scale = self.running_var
+        with torch.no_grad():
+            sq, wq, bq = self._params(scale.detach().contiguous()) if x.is_cuda else _cpu_unsupported("RangeBN")
+        out = (x - mean.view(1, mean.size(0), 1, 1)) * sq.view(1, sq.size(0), 1, 1)
+        out = out * wq.view(1, wq.size(0), 1, 1)
+        out = out + bq.view(1, bq.size(0), 1, 1)
+        if out.size(3) == 1 and out.size(2) == 1:
+            out = out.squeeze(-1).squeeze(-1)
+        return out
+
+
+def _cpu_unsupported(what):
+    raise RuntimeError(f"qnn: {what} needs a ROCm device (the CPU fake-quant reference lives in oracle/)")
+
+
+# ============================================================ tree helpers (:508-610)
+def is_bn(m):
+    return isinstance(m, nn.BatchNorm2d) or isinstance(m, nn.BatchNorm1d)
+
+
+def is_quant(m):
+    return isinstance(m, QuantNode) or isinstance(m, QLinear) or isinstance(m, QConv2d)
+
+
+def recursive_apply(model, func, *args):
+    for m in model.children():
+        func(m, *args)
+        recursive_apply(m, func, *args)
+
+
+def set_bn_is_train(model, train, logger=None, reload_running_estimators=False, reset_running_estimators=False,
+                    freeze_affine=False):
+    def func(m, *args):
+        if is_bn(m):
+            if reload_running_estimators or reset_running_estimators:
+                if (reload_running_estimators and not hasattr(m, "locked_running_mean")) or reset_running_estimators:
+                    m.locked_running_mean = m.running_mean.data.clone()
+                    m.locked_running_var = m.running_var.data.clone()
+                else:
+                    m.running_mean.data = m.locked_running_mean.clone()
+                    m.running_var.data = m.locked_running_var.clone()
+            if freeze_affine:
+                for p in m.parameters():
+                    p.requires_grad = False
+            m.train(train)
+
+    recursive_apply(model, func)
+
+
+def set_measure_mode(model, measure, momentum=None, logger=None):
+    def func(m, *args):
+        if is_bn(m):
+            m.train(not measure)
+        elif is_quant(m):
+            m.set_measure_mode(measure, momentum=momentum)
+
+    recursive_apply(model, func)
+
+
+def set_quant_mode(model, quant, logger=None):
+    def func(m, *args):
+        if is_quant(m):
+            m.enable_quant = quant
+
+    recursive_apply(model, func)
+
+
+def overwrite_params(model, logger=None):
+    def func(m, *args):
+        if is_quant(m):
+            m.overwrite_params(logger)
+
+    recursive_apply(model, func)
+
+
+def freeze_quant_params(model, freeze=True, include_param_dyn_range=True, momentum="same", logger=None):
+    """quantize.py:579-592.  Note: the reference sets `freeze_param_dyn_rang` (sic,
+    :590), so the weight range is never actually frozen; mirrored for parity."""
+
+    def func(m, *args):
+        if isinstance(m, QuantMeasure):
+            m.train(not freeze)
+            if momentum != "same":
+                m.momentum = momentum
+        if include_param_dyn_range and isinstance(m, QuantNode):
+            m.freeze_param_dyn_rang = freeze
+
+    recursive_apply(model, func)
+
+
+def distill_set_train(model, train):
+    model.train(train)
+    if train:
+        freeze_quant_params(model)
+        set_bn_is_train(model, False)
+
+
+def set_global_quantization_method(model, method="aciq", logger=None):
+    assert method in QuantMeasure._QMEASURE_SUPPORTED_METHODS
+
+    def func(m, *args):
+        if isinstance(m, QuantMeasure):
+            m.method = method
+
+    recursive_apply(model, func)

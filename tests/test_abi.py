@@ -1,0 +1,92 @@
+"""The C-ABI library loads, exports every symbol include/qnn.h declares, and
+validates arguments before touching the device (CPU-only checks)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import PKG, REPO
+
+HEADER = os.path.join(REPO, "include", "qnn.h")
+LIB = os.path.join(PKG, "qnn", "libqnn_hip.so")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(qnn_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", PKG, "-j8"], check=True, capture_output=True)
+    from qnn import _lib
+    return _lib.load()
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("qnn_qconv2d_fwd", "qnn_pack_weight_i8", "qnn_quantize_nchw_to_nhwc8", "qnn_fake_quant_f32",
+              "qnn_rangebn_f32", "qnn_dwconv2d_fwd", "qnn_last_error", "qnn_abi_version"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], check=True, capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\sT\s(qnn_\w+)", out))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+
+
+def test_bindings_cover_every_symbol(lib):
+    from qnn import _lib
+    for s in declared_symbols():
+        if s in ("qnn_last_error", "qnn_abi_version"):
+            continue
+        assert s in _lib.SIGNATURES, s
+
+
+def test_abi_version(lib):
+    assert lib.qnn_abi_version() == 1
+
+
+def test_argument_validation_without_device(lib):
+    # invalid arguments are rejected before any HIP call, with a message
+    rc = lib.qnn_fake_quant_f32(None, None, 16, 0.0, 0.0, 0.0, 255.0, None)
+    assert rc == 1
+    assert b"scale" in lib.qnn_last_error() or b"null" in lib.qnn_last_error()
+    rc = lib.qnn_qconv2d_fwd(None, 1, 8, 8, 17, None, 64, 64, 3, 3, 1, 1, 1, 1, 8, 8, None, None, None, None, None, 1,
+                             None, None, 0, None)
+    assert rc == 1 and b"cp" in lib.qnn_last_error()
+    rc = lib.qnn_qconv2d_fwd(None, 1, 8, 8, 16, None, 64, 64, 3, 3, 1, 1, 1, 1, 7, 8, None, None, None, None, None, 1,
+                             None, None, 0, None)
+    assert rc == 1 and b"ho/wo" in lib.qnn_last_error()
+    rc = lib.qnn_fake_quant_vec_f32(None, None, 70000, 255.0, 0, None, None)
+    assert rc == 1
+    # empty batches are a no-op success
+    assert lib.qnn_fake_quant_f32(None, None, 0, 0.0, 0.0, 1.0, 255.0, None) == 0
+
+
+def test_error_is_thread_local(lib):
+    import threading
+    lib.qnn_fake_quant_vec_f32(None, None, 0, 255.0, 0, None, None)
+    mine = lib.qnn_last_error()
+    seen = []
+
+    def other():
+        seen.append(lib.qnn_last_error())
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert mine and seen == [b""]
+
+
+def test_built_for_gfx950_only():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", LIB], capture_output=True, text=True)
+    blob = open(LIB, "rb").read()
+    assert b"gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob

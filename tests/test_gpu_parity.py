@@ -1,0 +1,232 @@
+"""GPU parity of the HIP path against the oracle and the reference's golden outputs.
+
+Tolerances:
+  * quantizer outputs / codes / packed weights: bit-exact;
+  * one layer on identical inputs: max|dy| <= 1e-5 * max|y_ref| + 1e-6 (the int32
+    contraction is exact; the error is fp32 epilogue rounding vs oneDNN's fp32 sum);
+  * whole model: max|dlogit| <= 3e-2 * max|logit_ref| and top-1 agreement
+    (a 1-ulp conv difference can flip a downstream round()).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import GOLDEN, load_fixture
+from fixtures_util import build_layer, build_model, oracle_layer
+from oracle import qnn_oracle as O
+from qnn import _lib, synthetic
+from qnn.quantize import QConv2d, QLinear, RangeBN, quantize, set_measure_mode
+
+pytestmark = pytest.mark.gpu
+
+LAYER_TOL = 1e-5
+LAYERS = sorted(os.path.basename(p)[6:-4] for p in glob.glob(os.path.join(GOLDEN, "layer_*.npz")))
+MODELS = sorted(os.path.basename(p)[6:-4] for p in glob.glob(os.path.join(GOLDEN, "model_*.npz")))
+
+
+def _close(y, ref, tol=LAYER_TOL):
+    y, ref = y.detach().float().cpu(), ref.detach().float().cpu()
+    assert y.shape == ref.shape
+    err = (y - ref).abs().max().item()
+    bound = tol * ref.abs().max().item() + 1e-6
+    assert err <= bound, f"max|dy|={err:.3e} > {bound:.3e} (max|y|={ref.abs().max().item():.3e})"
+    return err
+
+
+# ------------------------------------------------------------------ quantizer: bit-exact
+def test_fake_quant_float_range_kat(gpu):
+    d = load_fixture("quantize_kat")
+    i = 0
+    while f"float/{i}/x" in d:
+        x = torch.from_numpy(d[f"float/{i}/x"]).to(gpu)
+        mn, mx = d[f"float/{i}/range"]
+        y = quantize(x, 8, float(mn), float(mx)).cpu().numpy()
+        np.testing.assert_array_equal(y.view(np.uint32), d[f"float/{i}/y"].view(np.uint32))
+        i += 1
+
+
+def test_fake_quant_tensor_and_none_kat(gpu):
+    d = load_fixture("quantize_kat")
+    i = 0
+    while f"tensor/{i}/x" in d:
+        w = torch.from_numpy(d[f"tensor/{i}/x"]).to(gpu)
+        sh = (w.shape[0],) + (1,) * (w.dim() - 1)
+        y = quantize(w, 8, w.flatten(1).min(-1)[0].view(sh), w.flatten(1).max(-1)[0].view(sh))
+        np.testing.assert_array_equal(y.cpu().numpy(), d[f"tensor/{i}/y"])
+        i += 1
+    j = 0
+    while f"none/{j}/x" in d:
+        y = quantize(torch.from_numpy(d[f"none/{j}/x"]).to(gpu), num_bits=8)
+        np.testing.assert_array_equal(y.cpu().numpy(), d[f"none/{j}/y"])
+        j += 1
+
+
+@pytest.mark.parametrize("shape,c_pad", [((3, 24, 9, 11), 32), ((2, 3, 33, 17), 16), ((4, 64, 56, 56), 64)])
+def test_activation_codes_nhwc8(gpu, shape, c_pad):
+    x = synthetic.input_batch(shape, 5) * 2.0
+    mn, mx = -1.5, 3.25
+    q = torch.empty((shape[0], shape[2], shape[3], c_pad), dtype=torch.int8, device=gpu)
+    s = max((mx - mn) / 255.0, 1e-8)
+    xd = x.to(gpu)
+    _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(xd), _lib.ptr(q), shape[0], shape[1], shape[2], shape[3], c_pad,
+              -mn, s, 255.0, _lib.stream_of(xd))
+    ref = O.quantize_codes_np(x.numpy(), mn, mx).astype(np.int32) - 128  # N C H W
+    got = q.cpu().numpy().astype(np.int32)
+    np.testing.assert_array_equal(got[..., : shape[1]], ref.transpose(0, 2, 3, 1))
+    assert np.all(got[..., shape[1]:] == 0)
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 3, 3), (40, 24, 3, 3), (64, 3, 7, 7), (1000, 512, 1, 1)])
+def test_weight_pack_bitexact(gpu, shape):
+    w = torch.from_numpy(synthetic.normal(shape, 9, 0, 0.05))
+    w[1] = 0.25  # constant channel -> scale floor
+    cout, cin, kh, kw = shape
+    cin_pad = (cin + 15) // 16 * 16
+    cout_pad = (cout + 127) // 128 * 128
+    kpad = (kh * kw * cin_pad + 63) // 64 * 64
+    wd = w.to(gpu)
+    wq = torch.empty((cout_pad, kpad), dtype=torch.int8, device=gpu)
+    f = lambda *s: torch.empty(s, dtype=torch.float32, device=gpu)
+    s_w, b_w, tap, what, wmin, wmax = f(cout), f(cout), f(cout, kh * kw), f(cout, cin * kh * kw), f(cout), f(cout)
+    _lib.call("qnn_pack_weight_i8", _lib.ptr(wd), cout, cin, kh, kw, cin_pad, cout_pad, 255.0, None, None,
+              _lib.ptr(wq), _lib.ptr(s_w), _lib.ptr(b_w), _lib.ptr(tap), _lib.ptr(what), _lib.ptr(wmin),
+              _lib.ptr(wmax), _lib.stream_of(wd))
+    lo, hi = O.weight_ranges(w)
+    codes = O.codes_tensor_range(w, lo, hi).to(torch.int32) - 128            # [cout][cin][kh][kw]
+    packed = wq.cpu().to(torch.int32)[:cout, : kh * kw * cin_pad].view(cout, kh, kw, cin_pad)
+    assert torch.equal(packed[..., :cin], codes.permute(0, 2, 3, 1))
+    assert int(packed[..., cin:].abs().sum()) == 0 and int(wq.cpu()[cout:].abs().sum()) == 0
+    w_hat = O.uniform_quantize(w, 8, lo, hi)
+    np.testing.assert_array_equal(what.cpu().numpy(), w_hat.reshape(cout, -1).numpy())
+    np.testing.assert_array_equal(wmin.cpu().numpy(), lo.reshape(-1).numpy())
+    np.testing.assert_array_equal(wmax.cpu().numpy(), hi.reshape(-1).numpy())
+    ref_tap = w_hat.double().sum(1).reshape(cout, kh * kw).float()
+    torch.testing.assert_close(tap.cpu(), ref_tap, rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------------ layers vs golden + oracle
+@pytest.mark.parametrize("name", LAYERS)
+def test_layer_vs_reference_golden(gpu, name):
+    d = load_fixture("layer_" + name)
+    wrap, m, x = build_layer(d)
+    wrap = wrap.to(gpu)
+    with torch.no_grad():
+        y = wrap(x.to(gpu))
+    _close(y, torch.from_numpy(d["y"]))
+    if isinstance(m, (QConv2d, QLinear)):
+        # weight_min/max buffers are refreshed as the reference does
+        ref_lo, ref_hi = O.weight_ranges(m.weight.detach().cpu())
+        assert torch.equal(m.weight_min.cpu(), ref_lo) and torch.equal(m.weight_max.cpu(), ref_hi)
+
+
+CONV_CASES = [
+    # (cin, cout, k, stride, pad, groups, bias, N, H, W)
+    (256, 256, 3, 1, 1, 1, False, 4, 14, 14),     # headline ResNet-50 layer3 3x3
+    (64, 64, 3, 1, 1, 1, False, 2, 56, 56),       # ResNet-18 layer1
+    (3, 64, 7, 2, 3, 1, False, 2, 224, 224),      # stem
+    (1024, 256, 1, 1, 0, 1, False, 4, 14, 14),    # bottleneck 1x1 reduce
+    (512, 2048, 1, 1, 0, 1, False, 2, 7, 7),      # bottleneck 1x1 expand (cout 2048)
+    (256, 512, 1, 2, 0, 1, False, 4, 14, 14),     # strided downsample
+    (96, 80, 3, 2, 1, 1, True, 3, 15, 13),        # ragged, odd sizes, bias
+    (128, 128, 3, 2, 1, 128, True, 4, 28, 28),    # depthwise s2
+    (32, 32, 3, 1, 1, 32, True, 2, 112, 112),     # depthwise s1 (mobilenet first block)
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_vs_oracle(gpu, case):
+    cin, cout, k, st, pd, g, bias, N, H, W = case
+    m = QConv2d(cin, cout, k, stride=st, padding=pd, groups=g, bias=bias, num_bits_grad=8, biprecision=True)
+    wrap = nn.Sequential(m)
+    synthetic.init_params(wrap, 3)
+    m.quantize_input.running_min.fill_(0.0)
+    m.quantize_input.running_max.fill_(2.75)
+    wrap.eval()
+    x = synthetic.input_batch((N, cin, H, W), 17, relu=True) * 1.1
+    sd = {kk: v.clone() for kk, v in wrap.state_dict().items()}
+    ref = O.qconv2d(x, sd["0.weight"], sd.get("0.bias"), st, pd, 1, g, (0.0, 2.75))
+    with torch.no_grad():
+        y = wrap.to(gpu)(x.to(gpu))
+    _close(y, ref)
+
+
+def test_linear_vs_oracle(gpu):
+    m = QLinear(2048, 1000, num_bits_grad=8, biprecision=True)
+    wrap = nn.Sequential(m)
+    synthetic.init_params(wrap, 4)
+    m.quantize_input.running_min.fill_(0.0)
+    m.quantize_input.running_max.fill_(1.5)
+    wrap.eval()
+    x = synthetic.input_batch((37, 2048), 18, relu=True) * 0.6
+    sd = {kk: v.clone() for kk, v in wrap.state_dict().items()}
+    ref = O.qlinear(x, sd["0.weight"], sd["0.bias"], (0.0, 1.5))
+    with torch.no_grad():
+        y = wrap.to(gpu)(x.to(gpu))
+    _close(y, ref)
+
+
+def test_rangebn_bitexact_given_input(gpu):
+    d = load_fixture("layer_rbn_32")
+    wrap, m, x = build_layer(d)
+    ref = oracle_layer(O, d, wrap, x)
+    with torch.no_grad():
+        y = wrap.to(gpu)(x.to(gpu))
+    np.testing.assert_array_equal(y.cpu().numpy(), ref.numpy())
+
+
+# ------------------------------------------------------------------ models end to end
+@pytest.mark.parametrize("name", MODELS)
+def test_model_vs_reference_golden(gpu, name):
+    d = load_fixture("model_" + name)
+    model, x = build_model(d)
+    model = model.to(gpu)
+    with torch.no_grad():
+        logits = model(x.to(gpu)).cpu()
+    ref = torch.from_numpy(d["logits"])
+    err = (logits - ref).abs().max().item()
+    assert err <= 3e-2 * ref.abs().max().item(), (err, ref.abs().max().item())
+    assert torch.equal(logits.argmax(1), ref.argmax(1))
+
+
+# ------------------------------------------------------------------ behaviour
+def test_cpu_input_fails_loudly():
+    m = QConv2d(16, 16, 3, padding=1).eval()
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m(torch.randn(1, 16, 8, 8))
+
+
+def test_per_channel_false_raises_like_reference(gpu):
+    m = QConv2d(16, 16, 3, padding=1, per_channel=False).to(gpu).eval()
+    with pytest.raises(TypeError):
+        m(torch.randn(1, 16, 8, 8, device=gpu))
+
+
+def test_measure_mode_is_float_conv_and_calibrates(gpu):
+    m = QConv2d(16, 8, 3, padding=1).to(gpu)
+    wrap = nn.Sequential(m)
+    set_measure_mode(wrap, True)
+    wrap.train()
+    x = torch.randn(4, 16, 8, 8, device=gpu)
+    y = wrap(x)
+    torch.testing.assert_close(y, torch.nn.functional.conv2d(x, m.weight, m.bias, 1, 1))
+    lo = x.view(4, -1).min(-1)[0].mean()
+    assert m.quantize_input.num_measurements.item() == 1
+    torch.testing.assert_close(m.quantize_input.running_min, lo.view(1))  # first update: momentum 0/(0+1)
+
+
+def test_pack_cache_tracks_weight_updates(gpu):
+    m = QConv2d(32, 32, 3, padding=1, bias=False).to(gpu).eval()
+    m.quantize_input.running_min.fill_(-1.0)
+    m.quantize_input.running_max.fill_(1.0)
+    x = torch.randn(2, 32, 8, 8, device=gpu)
+    y1 = m(x)
+    with torch.no_grad():
+        m.weight.mul_(-1.0)
+    y2 = m(x)
+    assert not torch.allclose(y1, y2)
+    ref = O.qconv2d(x.cpu(), m.weight.detach().cpu(), None, 1, 1, 1, 1, (-1.0, 1.0))
+    _close(y2, ref)
