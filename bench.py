@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: images/sec of the 8-bit ResNet-18 eval forward on MI355X (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): resnet_quantized depth=18, ImageNet shape
+3x224x224, batch 128 per GPU, int8 MFMA path, synthetic inputs resident in HBM.
+A "step" is one forward of one batch (plus, at N>1, the RCCL gather of the
+logits to rank 0).  Weak scaling: every rank processes its own 128 images.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (see DESIGN.md §Measurement for every field).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "quantized.pytorch_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec, 8-bit ResNet-18 224×224 @1/2/4/8 GPU; % int8-MFMA roofline"
+PEAK_INT8_TOPS = 5000.0   # dense int8 MFMA, 256 CU x 2.4 GHz (MI355X_MICROARCH.md: 2x bf16 2.5 PF)
+PEAK_HBM_GBS = 8000.0
+
+
+def model_ops(model, batch, hw=224):
+    """Algorithmic int8 ops per forward: sum over QConv2d/QLinear of 2*N*Cout*Ho*Wo*Cin/g*kh*kw
+    (SURVEY.md §8(d)); returned as (total, mfma_part) where mfma_part excludes depthwise."""
+    from qnn.quantize import QConv2d, QLinear
+    shapes = {}
+    hooks = []
+
+    def rec(m, inp, out):
+        shapes[m] = (tuple(inp[0].shape), tuple(out.shape))
+
+    for m in model.modules():
+        if isinstance(m, (QConv2d, QLinear)):
+            hooks.append(m.register_forward_hook(rec))
+    with torch.no_grad():
+        model(torch.zeros(1, 3, hw, hw, device=next(model.parameters()).device))
+    for h in hooks:
+        h.remove()
+    total = mfma = 0
+    for m, (ishape, oshape) in shapes.items():
+        if isinstance(m, QLinear):
+            ops = 2 * batch * m.out_features * m.in_features
+        else:
+            kh, kw = m.kernel_size
+            ops = 2 * batch * m.out_channels * oshape[2] * oshape[3] * (m.in_channels // m.groups) * kh * kw
+        total += ops
+        if isinstance(m, QLinear) or m.groups == 1:
+            mfma += ops
+    return total, mfma
+
+
+def calibrate(model, device, seed, batches=2, bsz=16):
+    from qnn import synthetic
+    from qnn.quantize import set_measure_mode
+    set_measure_mode(model, True)
+    model.train()
+    with torch.no_grad():
+        for j in range(batches):
+            model(synthetic.input_batch((bsz, 3, 224, 224), seed + j).to(device))
+    set_measure_mode(model, False)
+    model.eval()
+
+
+def build(device, depth, seed=11):
+    from qnn import synthetic
+    from qnn.resnet_quantized import resnet_quantized
+    torch.manual_seed(0)
+    model = resnet_quantized(depth=depth, dataset="imagenet")
+    synthetic.init_params(model, seed)
+    model = model.to(device)
+    calibrate(model, device, 300)
+    return model
+
+
+def cpu_baseline(model_cpu_sd, depth, batch, iters, threads):
+    """Oracle (the reference's fake-quant CPU forward, restated) on a bounded sample."""
+    from oracle import qnn_oracle as O
+    from qnn import synthetic
+    torch.set_num_threads(threads)
+    x = synthetic.input_batch((batch, 3, 224, 224), 4242)
+    sd = {k: v.clone() for k, v in model_cpu_sd.items()}
+    kw = dict(depth=depth, dataset="imagenet")
+    O.model_forward(sd, x, "resnet", kw)  # warm-up
+    times = []
+    t_end = time.perf_counter() + 30.0
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        O.model_forward(sd, x, "resnet", kw)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() > t_end:
+            break
+    med = float(np.median(times))
+    return {"value": round(batch / med, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/qnn_oracle.py resnet{depth} imagenet fake-quant forward (biprecision double conv, "
+                      f"as the reference), batch {batch}, median of {len(times)} after 1 warm-up, "
+                      f"torch {torch.__version__} CPU, {threads} threads, {platform.processor() or platform.machine()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--depth", type=int, default=18)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-iters", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from qnn import _lib
+    from qnn import dist as qdist
+    rank, local_rank, world = qdist.init()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    _lib.load()
+
+    model = build(device, args.depth)
+    total_ops, mfma_ops = model_ops(model, args.batch)
+    from qnn import synthetic
+    x = synthetic.input_batch((args.batch, 3, 224, 224), 1234 + rank).to(device)
+    runner = qdist.ShardedInference(model, args.batch * world)
+
+    def step():
+        return runner(x)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # Per-launch HIP-event timing of the MFMA conv kernel over a few extra forwards
+    timer = _lib.LaunchTimer(["qnn_qconv2d_fwd"])
+    _lib.set_timer(timer)
+    reps = 3
+    with torch.no_grad():
+        for _ in range(reps):
+            model(x)
+    _lib.set_timer(None)
+    d = timer.durations_ms()
+    conv_ms_per_fwd = sum(ms for _, ms in d) / reps
+    launches = len(d) // reps
+
+    if rank == 0:
+        images = args.batch * world * args.steps
+        ms_per_step = elapsed / args.steps * 1e3
+        achieved = mfma_ops / (conv_ms_per_fwd * 1e-3) / 1e12
+        line = {
+            "metric": METRIC,
+            "value": round(images / elapsed, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic (N(0,1) 3x224x224 on device; numpy-PCG64 weights, reference init law)",
+            "config": {"workload": f"resnet_quantized depth={args.depth} imagenet eval forward, int8 MFMA path",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "parallelism": f"dp{world}", "model_gop_per_batch": round(total_ops / 1e9, 2)},
+            "roofline": {"bound": "mfma", "kernel": "qconv_mfma_kernel (all QConv2d/QLinear launches of one forward)",
+                         "achieved": round(achieved, 2), "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_INT8_TOPS, 4), "traffic": None,
+                         "launches_per_forward": launches, "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
+                         "model_frac": round(total_ops / (ms_per_step * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4)},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(16, len(os.sched_getaffinity(0)))
+            sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+            line["cpu_baseline"] = cpu_baseline(sd, args.depth, args.cpu_batch, args.cpu_iters, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

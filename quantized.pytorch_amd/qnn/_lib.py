@@ -75,10 +75,43 @@ def load(path=None):
     return lib
 
 
+class LaunchTimer:
+    """Optional per-launch HIP-event timing of selected entry points (bench/profiling).
+
+    Events are recorded on the current PyTorch stream, which is the stream every
+    qnn call is issued on, so they bracket exactly that launch.
+    """
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.records = []
+
+    def durations_ms(self):
+        torch.cuda.synchronize()
+        return [(n, a.elapsed_time(b)) for n, a, b in self.records]
+
+
+_timer = None
+
+
+def set_timer(timer):
+    global _timer
+    _timer = timer
+
+
 def call(name, *args):
     """Invoke a C-ABI entry point and raise QnnError on a non-zero status."""
     lib = load()
-    rc = getattr(lib, name)(*args)
+    t = _timer
+    if t is not None and name in t.names:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib, name)(*args)
+        e1.record()
+        t.records.append((name, e0, e1))
+    else:
+        rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.qnn_last_error().decode(errors="replace")
         raise QnnError(f"{name} failed (status {rc}): {msg}")

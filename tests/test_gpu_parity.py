@@ -4,8 +4,12 @@ Tolerances:
   * quantizer outputs / codes / packed weights: bit-exact;
   * one layer on identical inputs: max|dy| <= 1e-5 * max|y_ref| + 1e-6 (the int32
     contraction is exact; the error is fp32 epilogue rounding vs oneDNN's fp32 sum);
-  * whole model: max|dlogit| <= 3e-2 * max|logit_ref| and top-1 agreement
-    (a 1-ulp conv difference can flip a downstream round()).
+  * every layer inside each model, teacher-forced on the input the GPU forward fed
+    it: the per-layer bar above (RangeBN bit-exact);
+  * whole model: max|dlogit| <= max(3e-2 * max|logit_ref|, 1.5 * drift64), where
+    drift64 is the reference's own logit change when its contraction runs in fp64
+    (a 1-ulp conv difference can flip a downstream round(), SURVEY.md §0.6);
+    top-1 equal wherever the reference's top-1 margin exceeds 2 * drift64.
 """
 import glob
 import os
@@ -16,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from conftest import GOLDEN, load_fixture
-from fixtures_util import build_layer, build_model, oracle_layer
+from fixtures_util import build_layer, build_model, e2e_tolerance, oracle_fp64_drift, oracle_layer
 from oracle import qnn_oracle as O
 from qnn import _lib, synthetic
 from qnn.quantize import QConv2d, QLinear, RangeBN, quantize, set_measure_mode
@@ -180,16 +184,55 @@ def test_rangebn_bitexact_given_input(gpu):
 
 # ------------------------------------------------------------------ models end to end
 @pytest.mark.parametrize("name", MODELS)
-def test_model_vs_reference_golden(gpu, name):
+def test_model_layers_teacher_forced(gpu, name):
+    """Every QConv2d / QLinear / RangeBN of the model, on the exact input it sees
+    inside the GPU forward, against the oracle layer: the tight per-layer bar in
+    model context (RangeBN bit-exact given its input)."""
     d = load_fixture("model_" + name)
     model, x = build_model(d)
     model = model.to(gpu)
+    seen = []
+    hooks = [m.register_forward_hook(lambda m, i, o: seen.append((m, i[0].detach().cpu(), o.detach().cpu())))
+             for m in model.modules() if isinstance(m, (QConv2d, QLinear, RangeBN))]
     with torch.no_grad():
-        logits = model(x.to(gpu)).cpu()
+        model(x.to(gpu))
+    for h in hooks:
+        h.remove()
+    assert len(seen) > 20
+    worst = 0.0
+    for m, xin, yout in seen:
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        rng = O.measure_range(sd, "quantize_input.")
+        if isinstance(m, RangeBN):
+            ref = O.rangebn(xin, sd["running_mean"], sd["running_var"], sd["weight"], sd["bias"], rng)
+            assert torch.equal(yout, ref)
+            continue
+        if isinstance(m, QLinear):
+            ref = O.qlinear(xin, sd["weight"], sd.get("bias"), rng)
+        else:
+            ref = O.qconv2d(xin, sd["weight"], sd.get("bias"), m.stride, m.padding, 1, m.groups, rng)
+        worst = max(worst, _close(yout, ref) / ref.abs().max().item())
+    print(f"{name}: {len(seen)} layers, worst max|dy|/max|y| = {worst:.2e}")
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_model_vs_reference_golden(gpu, name):
+    """Statistical end-to-end bar: within 1.5x the reference's own fp64-vs-fp32
+    contraction drift (floor 3%), top-1 equal wherever the reference's own top-1
+    margin exceeds that drift."""
+    d = load_fixture("model_" + name)
+    model, x = build_model(d)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
     ref = torch.from_numpy(d["logits"])
+    drift64, _ = oracle_fp64_drift(O, sd, x, d["config"]["factory"], d["config"]["kw"], ref)
+    with torch.no_grad():
+        logits = model.to(gpu)(x.to(gpu)).cpu()
     err = (logits - ref).abs().max().item()
-    assert err <= 3e-2 * ref.abs().max().item(), (err, ref.abs().max().item())
-    assert torch.equal(logits.argmax(1), ref.argmax(1))
+    tol = e2e_tolerance(ref, drift64)
+    assert err <= tol, (err, tol, drift64)
+    top2 = ref.topk(2, dim=1).values
+    decisive = (top2[:, 0] - top2[:, 1]) > 2 * drift64
+    assert torch.equal(logits.argmax(1)[decisive], ref.argmax(1)[decisive])
 
 
 # ------------------------------------------------------------------ behaviour
