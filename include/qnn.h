@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 1
+#define QNN_ABI_VERSION 2
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -69,23 +69,38 @@ int qnn_fake_quant_vec_f32(const float* x, float* y, int n, float qmax, int scal
 int qnn_fake_quant_rows_f32(const float* x, float* y, int rows, int64_t cols, const float* mins,
                             const float* maxs, float qmax, qnn_stream_t stream);
 
-/* Activation codes for the int8 path: NCHW fp32 -> NHWC8 (q - 128), channel pad 0.
- * The per-tensor QuantMeasure range (quantize.py:241-249) is (min, scale). */
-int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, int w, int cp,
+/* Activation codes for the int8 path: NCHW fp32 -> spatially padded NHWC8
+ * [n][h+2*pad][w+2*pad][cp] holding q - 128 (quantize.py:89-95 codes), with the
+ * border and channel padding written as code' 0 — zero padding of x_hat adds
+ * nothing to the exact decomposition — followed by a 128-byte
+ * zero tail (the conv's zero page, at byte offset n*(h+2p)*(w+2p)*cp).  The buffer
+ * must hold that many bytes + 128.  Range: QuantMeasure's (min, scale). */
+int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, int w, int pad, int cp,
                                float neg_min, float scale, float qmax, qnn_stream_t stream);
+
+/* Same codes in space-to-depth form for stride-2 convs on few channels (the
+ * 7x7/2 and 3x3/2 stems): z[n][h2][w2][(2u+v)*c + ci] = code(x[n][ci][2*h2+u-pad][2*w2+v-pad])
+ * (code' 0 outside the image), 4*c <= 16 = cpz, z is [n][hz][wz][16] + 128-byte zero tail.
+ * A kh x kw stride-2 conv becomes a ceil(kh/2) x ceil(kw/2) stride-1 conv on z. */
+int qnn_quantize_nchw_to_s2d8(const float* x, int8_t* z, int n, int c, int h, int w, int pad, int hz, int wz,
+                              float neg_min, float scale, float qmax, qnn_stream_t stream);
 
 /* Per-output-channel weight quantization + pre-pack for the int8 contraction.
  * Replaces QConv2d.forward :317-334 / QLinear.forward :401-415 (per_channel=True):
  *   weight_min/max = w.flatten(1).min/max(-1)   (or the given ones when frozen: w_min_in/w_max_in non-null)
  *   s_w = clamp(fl(fl(max-min)/qmax), 1e-8);  q_w = rint(clamp(fl(fl(w + (-min)) / s_w), 0, qmax))
- * Outputs (all device buffers):
- *   wq      [cout_pad][kh][kw][cin_pad] int8 codes q_w - 128 (zero in padding rows/channels)
- *   s_w     [cout]  fp32 scale;  b_w [cout] fp32 = 128*s_w + min (double-rounded once)
- *   tap_sum [cout][kh*kw] fp32 = sum_ci of the dequantized weights w_hat (fp64 accumulation)
+ * Packed rows (stride kpad = round_up(taps * cin_pad, 128) bytes, codes q_w - 128, zeros
+ * in every padding position and in rows >= cout):
+ *   s2d == 0: [cout_pad][kh][kw][cin_pad]
+ *   s2d == 2: [cout_pad][ceil(kh/2)][ceil(kw/2)][cin_pad] with channel (2u+v)*cin_g + ci
+ *             holding tap (2a+u, 2b+v) — the space-to-depth weights (cin_pad >= 4*cin_g).
+ * Other outputs (device buffers):
+ *   s_w [cout] fp32 scale;  b_w [cout] fp32 = 128*s_w + min (double-rounded once)
+ *   tap_sum [cout][kh*kw] fp32 = sum_ci of the dequantized weights w_hat, ORIGINAL taps
  *   w_hat   [cout][cin_g*kh*kw] fp32 dequantized weights (nullable)
  *   w_min_out / w_max_out [cout] (nullable): the ranges used (the reference stores them in
  *   the weight_min/weight_max buffers). */
-int qnn_pack_weight_i8(const float* w, int cout, int cin_g, int kh, int kw, int cin_pad, int cout_pad,
+int qnn_pack_weight_i8(const float* w, int cout, int cin_g, int kh, int kw, int cin_pad, int cout_pad, int s2d,
                        float qmax, const float* w_min_in, const float* w_max_in, int8_t* wq, float* s_w,
                        float* b_w, float* tap_sum, float* w_hat, float* w_min_out, float* w_max_out,
                        qnn_stream_t stream);
@@ -98,18 +113,60 @@ int qnn_conv_border_table(const float* tap_sum, int cout, int kh, int kw, const 
 
 /* ---------------------------------------------------------------- contraction */
 
-/* Eval forward of QConv2d (quantize.py:314-349; biprecision's out1+out2-out1 is
- * bitwise one conv) on pre-quantized operands, int8 MFMA
- * implicit GEMM (v_mfma_i32_32x32x32_i8), exact int32 accumulation, fp32 epilogue:
- *   y[n][c][p] = sxsw[c]*acc + sxbw[c]*sum_valid(q'_x) + table[hcls[ho]][wcls[wo]][c] + bias[c]
- * with sxsw = s_x*s_w, sxbw = s_x*b_w.  groups must be 1 (depthwise: qnn_dwconv2d_fwd).
- * x: NHWC8 [n][h][w][cp]; wq: from qnn_pack_weight_i8 (cin_pad == cp).
- * out_layout 0: y is NCHW fp32 [n][cout][ho][wo]; 1: y is NHWC fp32 [n][ho][wo][cout].
- * bias nullable (already fake-quantized, quantize.py:336-340). */
-int qnn_qconv2d_fwd(const int8_t* x, int n, int h, int w, int cp, const int8_t* wq, int cout,
-                    int cout_pad, int kh, int kw, int sh, int sw, int ph, int pw, int ho, int wo,
-                    const float* sxsw, const float* sxbw, const float* table, const int* hcls,
-                    const int* wcls, int nwc, const float* bias, float* y, int out_layout,
+/* Geometry of one int8 contraction over a spatially pre-padded NHWC8 input. */
+typedef struct qnn_conv_desc {
+  int n, hp, wp, cp;   /* input codes [n][hp][wp][cp], cp = 16 * 2^j, border = code' 0   */
+  int zero_off;        /* byte offset from x of >= 16 zero bytes (reads past K land here)  */
+  int cout, cout_pad;  /* output channels; packed weight rows (>= round_up(cout, 64|128))  */
+  int kh, kw, sh, sw;  /* taps and strides in the padded input's coordinates               */
+  int ho, wo;          /* output pixel (ho, wo) reads input rows ho*sh + r, cols wo*sw + s */
+  int kpad;            /* packed weight row stride in bytes (multiple of 128)              */
+} qnn_conv_desc;
+
+/* Epilogue of the contraction.  Always:
+ *   y = sxsw[c]*acc + sxbw[c]*sum_valid(q'_x) + table[hcls[ho]*nwc + wcls[wo]][c] (+ bias[c])
+ * (exact decomposition; table = b_x * border-aware sum of w_hat, from
+ * qnn_conv_border_table over the ORIGINAL unpadded geometry).
+ * mode 0 (drop-in): out_f32 = y as NCHW fp32 [n][cout][ho][wo] — QConv2d.forward's output.
+ * mode 1 (fused model graph, resnet_quantized.py:52-68/:93-113, mobilenet_quantized.py:38-48):
+ *   v = bn_mean ? RangeBN_eval(y) : y     (quantize.py:461-499, exact fp32 op order;
+ *                                          out_bncode receives RangeBN's input code)
+ *   v = residual ? fl(v + residual) : v   (NHWC fp32 [m][cout])
+ *   v = relu ? max(v, 0) : v
+ *   out_f32 = v (NHWC fp32 [m][cout]);  out_code{0,1} = codes of v for a consumer conv with
+ *   QuantMeasure range (neg_min, scale, qmax), written into that consumer's padded NHWC8
+ *   buffer [n][hp][wp][cp] at (ho + pad, wo + pad).  cout % 4 == 0. */
+typedef struct qnn_epilogue {
+  int mode;
+  const float* sxsw;
+  const float* sxbw;
+  const float* table;
+  const int* hcls;
+  const int* wcls;
+  int nwc, nclass;
+  const float* bias;
+  const float* bn_mean;
+  const float* bn_sq;
+  const float* bn_wq;
+  const float* bn_bq;
+  float bn_neg_min, bn_min, bn_scale, bn_qmax;
+  const float* residual;
+  int relu;
+  float* out_f32;
+  uint8_t* out_bncode;
+  int8_t* out_code0;
+  int code0_cp, code0_pad, code0_hp, code0_wp;
+  float code0_neg_min, code0_scale, code0_qmax;
+  int8_t* out_code1;
+  int code1_cp, code1_pad, code1_hp, code1_wp;
+  float code1_neg_min, code1_scale, code1_qmax;
+} qnn_epilogue;
+
+/* Eval forward of QConv2d / QLinear (quantize.py:314-349, :398-428; biprecision's
+ * out1 + out2 - out1 is bitwise one conv) on pre-quantized operands:
+ * int8 MFMA implicit GEMM (v_mfma_i32_32x32x32_i8), exact int32 accumulation, fp32
+ * epilogue as described by `epi`.  groups == 1 (depthwise: qnn_dwconv2d_fwd). */
+int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
                     qnn_stream_t stream);
 
 /* Depthwise (groups == cin == cout) eval forward: fake-quantize-on-load of x

@@ -1,264 +1,326 @@
-// int8 MFMA implicit-GEMM convolution for the eval forward of QConv2d / QLinear
-// (models/modules/quantize.py:314-349 and :398-428; biprecision is one contraction,
-// SURVEY.md §0.3).  CDNA4 / gfx950 only: v_mfma_i32_32x32x32_i8.
+// int8 MFMA implicit-GEMM convolution: the eval forward of QConv2d / QLinear
+// (models/modules/quantize.py:314-349, :398-428; biprecision's out1+out2-out1
+// is one contraction).  CDNA4 / gfx950: v_mfma_i32_32x32x32_i8.
 //
-// GEMM view:  D[c][m] = sum_k Wq'[c][k] * Xq'[k][m]
-//   c = output channel (MFMA rows, operand A = packed weights [cout_pad][kpad])
-//   m = output pixel n*Ho*Wo + ho*Wo + wo (MFMA columns, operand B gathered from
-//       the NHWC8 activation codes: implicit im2col, zero outside the image)
-//   k = (kh, kw, ci) tap-major, ci padded to Cp (16-byte chunks, one tap each)
-// Exact decomposition of the reference fp32 conv of dequantized operands
-// (SURVEY.md §0.5), evaluated in the epilogue:
-//   y = s_x*s_w[c]*acc + s_x*b_w[c]*sum_valid(q'_x) + b_x*sum_valid(w_hat[c]) (+ bias[c])
-// sum_valid(q'_x) is accumulated in-loop from the B fragments (v_dot4 against 1s);
-// the border-aware third term comes from a per-(row class, col class, c) table.
+// GEMM view  D[c][m] = sum_k Wq'[c][k] * Xq'[k][m]
+//   c: output channel  -> MFMA rows    (operand A: packed weights [cout_pad][kpad])
+//   m: output pixel    -> MFMA columns (operand B: implicit im2col of the NHWC8 codes)
+//   k: (kh, kw, ci) tap-major, ci padded to Cp = 16 * 2^j
+// The input is SPATIALLY PRE-PADDED ([n][hp][wp][cp], border code' = 0): zero
+// padding of x_hat contributes nothing to any term of the exact decomposition
+// (SURVEY.md §0.5), so the gather has no bounds checks at all and goes straight
+// HBM -> LDS with global_load_lds_dwordx4.  Chunks past K read a zero page.
 //
-// Block: 256 threads = 4 waves laid out WM x WN; each wave owns TM x TN tiles of
-// 32x32; BK = 64 bytes of K per LDS stage, double-buffered, register-staged
-// loads (issue early, write after compute), XOR-swizzled 16-B chunks so the
-// ds_read_b128 fragment reads are bank-conflict free.
+// Epilogue: y = s_x*s_w[c]*acc + s_x*b_w[c]*sum_valid(q'_x) + b_x*sum_valid(w_hat[c]) (+ bias)
+//   sum_valid(q'_x): v_dot4 of the B fragments against 1s (exact, in-loop);
+//   border term: per (row class, col class, c) table staged in LDS.
+// Then either the drop-in output (fp32 NCHW, the reference module boundary), or
+// the fused chain of the model graph: RangeBN eval (quantize.py:461-499, exact
+// fp32 op order) -> + residual -> ReLU -> fp32 NHWC and/or requantized NHWC8
+// codes for up to two consumer convs (their QuantMeasure ranges).
+//
+// Block: 256 threads = 4 waves, each wave a 64x64 tile (2x2 MFMA 32x32x32).
+// K stage = 128 bytes; two LDS stages filled by LDS-DMA, counted vmcnt, raw
+// s_barrier; rows XOR-swizzled so ds_read_b128 fragment reads are conflict-free.
 #include "qnn_internal.h"
 
 namespace qnn {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-struct ConvParams {
-  const int8_t* x;   // [N][H][W][Cp]
-  const int8_t* w;   // [cout_pad][kpad]
-  float* y;
-  const float* sxsw;
-  const float* sxbw;
-  const float* table;
-  const int* hcls;
-  const int* wcls;
-  const float* bias;
-  int N, H, W, Cp, Cout, KH, KW, SH, SW, PH, PW, Ho, Wo;
-  int K;     // KH*KW*Cp (real)
-  int kpad;  // packed row stride, multiple of 64
-  int M;     // N*Ho*Wo
-  int nwc;
-  int out_layout;
+constexpr int BK = 128;         // bytes of K per LDS stage (4 MFMA k-steps of 32)
+constexpr int MAX_TAPS = 64;
+constexpr int MAX_CLASSES = 64;
+
+struct Params {
+  qnn_conv_desc d;
+  qnn_epilogue e;
+  int M;        // n*ho*wo
+  int taps;     // kh*kw
+  int lgcpt;    // log2(cp/16)
+  int nstage;   // kpad / BK
 };
 
-constexpr int BK = 64;
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 2) & 3)) << 4); }
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
 
-template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(256) void qconv_mfma_kernel(const ConvParams p) {
-  constexpr int BM = WM * TM * 32;  // output channels per block
-  constexpr int BN = WN * TN * 32;  // output pixels per block
-  constexpr int A_LD = BM * 4 / 256;  // 16-B chunks per thread per stage
-  constexpr int B_LD = BN * 4 / 256;
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(A_LD >= 1 && B_LD >= 1, "tile too small");
+__device__ __forceinline__ void store_code4(int8_t* p, float4 v, float nm, float s, float qmax) {
+  int b0 = (int)quant_code(v.x, nm, s, qmax) - 128;
+  int b1 = (int)quant_code(v.y, nm, s, qmax) - 128;
+  int b2 = (int)quant_code(v.z, nm, s, qmax) - 128;
+  int b3 = (int)quant_code(v.w, nm, s, qmax) - 128;
+  *reinterpret_cast<int*>(p) = (b0 & 255) | ((b1 & 255) << 8) | ((b2 & 255) << 16) | ((b3 & 255) << 24);
+}
 
-  __shared__ __attribute__((aligned(16))) int8_t smem[2 * (BM + BN) * BK];
-  auto sA = [&](int b) { return smem + b * (BM * BK); };
-  auto sB = [&](int b) { return smem + 2 * BM * BK + b * (BN * BK); };
+template <int BM, int BN, bool FUSED>
+__global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+                                                    const Params p) {
+  constexpr int WM = BM / 64, WN = BN / 64;
+  static_assert(WM * WN == 4, "4 waves of 64x64");
+  constexpr int NA = BM / 32;  // glds per wave per stage for A (1 KiB = 8 rows each)
+  constexpr int NB = BN / 32;
+  constexpr int STAGE = (BM + BN) * BK;
+  // one LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * STAGE + 4 * MAX_TAPS];
+  int* s_tap = reinterpret_cast<int*>(smem + 2 * STAGE);
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.x * BN;
-  const int c0 = blockIdx.y * BM;
-  const int HoWo = p.Ho * p.Wo;
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
 
-  // ---- per-thread gather state for B (activation) chunks
-  const int8_t* bptr[B_LD];
-  int bh[B_LD], bw[B_LD];
-  int bci[B_LD], br[B_LD], bs[B_LD];
-  int bk[B_LD];
-#pragma unroll
-  for (int i = 0; i < B_LD; ++i) {
-    int q = tid + 256 * i;
-    int prow = q >> 2, cj = q & 3;
-    int m = m0 + prow;
-    if (m < p.M) {
-      int n = m / HoWo;
-      int hw = m - n * HoWo;
-      int ho = hw / p.Wo;
-      int wo = hw - ho * p.Wo;
-      bh[i] = ho * p.SH - p.PH;
-      bw[i] = wo * p.SW - p.PW;
-      bptr[i] = p.x + (int64_t)n * p.H * p.W * p.Cp;
-    } else {
-      bh[i] = -100000;  // never in bounds
-      bw[i] = 0;
-      bptr[i] = p.x;
-    }
-    // k = 16*cj within the first stage
-    int k = 16 * cj;
-    int tap = k / p.Cp;
-    bci[i] = k - tap * p.Cp;
-    br[i] = tap / p.KW;
-    bs[i] = tap - br[i] * p.KW;
-    bk[i] = k;
+  // ---- XCD-aware, bijective block -> tile map: each XCD gets a contiguous run of
+  // tiles, output-channel tiles fastest so blocks sharing an activation tile share L2
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nbx = (p.M + BN - 1) / BN;
+  const int nblk = nbx * nby;
+  int t;
+  {
+    const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
   }
-  const int8_t* aptr[A_LD];
-#pragma unroll
-  for (int i = 0; i < A_LD; ++i) {
-    int q = tid + 256 * i;
-    aptr[i] = p.w + (int64_t)(c0 + (q >> 2)) * p.kpad + 16 * (q & 3);
-  }
+  const int m0 = (t / nby) * BN;
+  const int c0 = (t % nby) * BM;
+  const int HoWo = d.ho * d.wo;
 
-  v4i ra[A_LD], rb[B_LD];
-  auto load_stage = [&](int k0) {
+  if (tid < p.taps) s_tap[tid] = ((tid / d.kw) * d.wp + (tid % d.kw)) * d.cp;
+
+  // ---- per-lane load state
+  uint32_t boff[NB];
+  int bchunk[NB];
 #pragma unroll
-    for (int i = 0; i < A_LD; ++i) ra[i] = *reinterpret_cast<const v4i*>(aptr[i] + k0);
+  for (int j = 0; j < NB; ++j) {
+    const int row = 8 * (wave + 4 * j) + (lane >> 3);
+    int m = m0 + row;
+    if (m > p.M - 1) m = p.M - 1;
+    const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
+    boff[j] = (uint32_t)(((n * d.hp + ho * d.sh) * d.wp + wo * d.sw) * d.cp);
+    bchunk[j] = (lane & 7) ^ ((row >> 1) & 7);
+  }
+  const int8_t* aptr[NA];
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      v4i v = {0, 0, 0, 0};
-      int hi = bh[i] + br[i], wi = bw[i] + bs[i];
-      if (bk[i] < p.K && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
-        v = *reinterpret_cast<const v4i*>(bptr[i] + ((int64_t)(hi * p.W + wi) * p.Cp + bci[i]));
-      rb[i] = v;
-      // advance this chunk's k by BK
-      bk[i] += BK;
-      bci[i] += BK;
-      while (bci[i] >= p.Cp) {
-        bci[i] -= p.Cp;
-        if (++bs[i] == p.KW) {
-          bs[i] = 0;
-          ++br[i];
-        }
-      }
-    }
-  };
-  auto store_stage = [&](int buf) {
+  for (int j = 0; j < NA; ++j) {
+    const int row = 8 * (wave + 4 * j) + (lane >> 3);
+    aptr[j] = w + (int64_t)(c0 + row) * d.kpad + 16 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  const int cpt_mask = (1 << p.lgcpt) - 1;
+  __syncthreads();  // s_tap
+
+  auto issue = [&](int st, int buf) {
+    int8_t* sa = smem + buf * STAGE;
+    int8_t* sb = sa + BM * BK;
 #pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      int q = tid + 256 * i;
-      *reinterpret_cast<v4i*>(sA(buf) + swz(q >> 2, q & 3)) = ra[i];
-    }
+    for (int j = 0; j < NA; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(aptr[j] + st * BK),
+                                       (lds_ptr_t)(sa + (wave + 4 * j) * 1024), 16, 0, 0);
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      int q = tid + 256 * i;
-      *reinterpret_cast<v4i*>(sB(buf) + swz(q >> 2, q & 3)) = rb[i];
+    for (int j = 0; j < NB; ++j) {
+      const int kc = st * 8 + bchunk[j];
+      const int tap = kc >> p.lgcpt;
+      uint32_t off = tap < p.taps ? boff[j] + (uint32_t)s_tap[tap] + (uint32_t)((kc & cpt_mask) << 4)
+                                  : (uint32_t)d.zero_off;
+      asm volatile("" : "+v"(off));  // keep ONE per-lane-address load (no saddr/vaddr branch split)
+      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wave + 4 * j) * 1024), 16, 0, 0);
     }
   };
 
-  v16i acc[TM][TN];
+  v16i acc[2][2];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (v16i){0};
-  int sumq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) sumq[j] = 0;
-
-  const int nstage = p.kpad / BK;
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
+    for (int j = 0; j < 2; ++j) acc[i][j] = (v16i){0};
+  int sumq[2] = {0, 0};
 
   const int frow = lane & 31, fh = lane >> 5;
-  for (int st = 0; st < nstage; ++st) {
+  issue(0, 0);
+  for (int st = 0; st < p.nstage; ++st) {
     const int buf = st & 1;
-    if (st + 1 < nstage) load_stage((st + 1) * BK);
+    if (st + 1 < p.nstage) {
+      issue(st + 1, buf ^ 1);
+      wait_vmcnt<NA + NB>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    const int8_t* sa = smem + buf * STAGE;
+    const int8_t* sb = sa + BM * BK;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < 4; ++ks) {
       const int chunk = 2 * ks + fh;
-      v4i fa[TM], fb[TN];
+      v4i fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        fa[i] = *reinterpret_cast<const v4i*>(sA(buf) + swz(wm * TM * 32 + i * 32 + frow, chunk));
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz(wm * 64 + i * 32 + frow, chunk));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        fb[j] = *reinterpret_cast<const v4i*>(sB(buf) + swz(wn * TN * 32 + j * 32 + frow, chunk));
-        int s = __builtin_amdgcn_sdot4(fb[j].x, 0x01010101, 0, false);
+      for (int j = 0; j < 2; ++j) {
+        fb[j] = *reinterpret_cast<const v4i*>(sb + swz(wn * 64 + j * 32 + frow, chunk));
+        int s = __builtin_amdgcn_sdot4(fb[j].x, 0x01010101, sumq[j], false);
         s = __builtin_amdgcn_sdot4(fb[j].y, 0x01010101, s, false);
         s = __builtin_amdgcn_sdot4(fb[j].z, 0x01010101, s, false);
-        s = __builtin_amdgcn_sdot4(fb[j].w, 0x01010101, s, false);
-        sumq[j] += s;
+        sumq[j] = __builtin_amdgcn_sdot4(fb[j].w, 0x01010101, s, false);
       }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (st + 1 < nstage) store_stage(buf ^ 1);
-    __syncthreads();
+    __builtin_amdgcn_s_barrier();
   }
 
-  // ---- epilogue
+  // ================================================================ epilogue
+  const qnn_epilogue& e = p.e;
+  float* s_f = reinterpret_cast<float*>(smem);  // main-loop LDS is free now
+  // [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq  [7BM..) table[cls][BM]
+  const int nparam = 7 * BM;
+  for (int i = tid; i < BM; i += 256) {
+    const int c = c0 + i;
+    const bool ok = c < d.cout;
+    s_f[i] = ok ? e.sxsw[c] : 0.f;
+    s_f[BM + i] = ok ? e.sxbw[c] : 0.f;
+    s_f[2 * BM + i] = (ok && e.bias) ? e.bias[c] : 0.f;
+    if (FUSED && e.bn_mean) {
+      s_f[3 * BM + i] = ok ? e.bn_mean[c] : 0.f;
+      s_f[4 * BM + i] = ok ? e.bn_sq[c] : 0.f;
+      s_f[5 * BM + i] = ok ? e.bn_wq[c] : 0.f;
+      s_f[6 * BM + i] = ok ? e.bn_bq[c] : 0.f;
+    }
+  }
+  for (int i = tid; i < e.nclass * BM; i += 256) {
+    const int cls = i / BM, c = c0 + (i - cls * BM);
+    s_f[nparam + i] = c < d.cout ? e.table[cls * d.cout + c] : 0.f;
+  }
+  __syncthreads();
 #pragma unroll
-  for (int j = 0; j < TN; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
+  for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
 
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int m = m0 + wn * TN * 32 + j * 32 + frow;
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + wn * 64 + j * 32 + frow;
     if (m >= p.M) continue;
-    const int n = m / HoWo;
-    const int hw = m - n * HoWo;
-    const int ho = hw / p.Wo;
-    const int wo = hw - ho * p.Wo;
-    const float* trow = p.table + (int64_t)(p.hcls[ho] * p.nwc + p.wcls[wo]) * p.Cout;
+    const int n = m / HoWo, hw = m - n * HoWo, ho = hw / d.wo, wo = hw - ho * d.wo;
+    const float* trow = s_f + nparam + (e.hcls[ho] * e.nwc + e.wcls[wo]) * BM;
     const float sq = (float)sumq[j];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < 2; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int c = c0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        if (c >= p.Cout) continue;
-        float v = fmaf(p.sxsw[c], (float)acc[i][j][r], fmaf(p.sxbw[c], sq, trow[c]));
-        if (p.bias) v = v + p.bias[c];
-        if (p.out_layout == 0)
-          p.y[((int64_t)n * p.Cout + c) * HoWo + hw] = v;
-        else
-          p.y[(int64_t)m * p.Cout + c] = v;
+      for (int g = 0; g < 4; ++g) {
+        const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g
+        const int c = c0 + cl;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int l = cl + u;
+          float y = fmaf(s_f[l], (float)acc[i][j][4 * g + u], fmaf(s_f[BM + l], sq, trow[l]));
+          v[u] = y + s_f[2 * BM + l];
+        }
+        if (!FUSED) {
+          float* yp = e.out_f32 + ((int64_t)n * d.cout + c) * HoWo + hw;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (c + u < d.cout) yp[(int64_t)u * HoWo] = v[u];
+          continue;
+        }
+        if (c >= d.cout) continue;  // cout % 4 == 0 in fused mode
+        if (e.bn_mean) {
+          int qb[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int l = cl + u;
+            const float q = quant_code(v[u], e.bn_neg_min, e.bn_scale, e.bn_qmax);  // RangeBN.quantize_input
+            qb[u] = (int)q;
+            float o = dequant(q, e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
+            o = o * s_f[4 * BM + l];                                         // * q(scale)
+            o = o * s_f[5 * BM + l];                                         // * q(weight)
+            v[u] = o + s_f[6 * BM + l];                                      // + q(bias)
+          }
+          if (e.out_bncode)
+            *reinterpret_cast<int*>(e.out_bncode + (int64_t)m * d.cout + c) =
+                qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24);
+        }
+        float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
+        if (e.residual) {
+          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + (int64_t)m * d.cout + c);
+          o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
+        }
+        if (e.relu) {
+          o4.x = fmaxf(o4.x, 0.f); o4.y = fmaxf(o4.y, 0.f); o4.z = fmaxf(o4.z, 0.f); o4.w = fmaxf(o4.w, 0.f);
+        }
+        if (e.out_f32) *reinterpret_cast<float4*>(e.out_f32 + (int64_t)m * d.cout + c) = o4;
+        if (e.out_code0) {
+          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
+          store_code4(e.out_code0 + a, o4, e.code0_neg_min, e.code0_scale, e.code0_qmax);
+        }
+        if (e.out_code1) {
+          const int64_t a = (((int64_t)n * e.code1_hp + ho + e.code1_pad) * e.code1_wp + wo + e.code1_pad) * e.code1_cp + c;
+          store_code4(e.out_code1 + a, o4, e.code1_neg_min, e.code1_scale, e.code1_qmax);
+        }
       }
     }
   }
 }
 
-template <int WM, int WN, int TM, int TN>
-static int launch(const ConvParams& p, hipStream_t stream) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  dim3 grid((unsigned)cdiv(p.M, BN), (unsigned)cdiv(p.Cout, BM));
-  hipLaunchKernelGGL((qconv_mfma_kernel<WM, WN, TM, TN>), grid, dim3(256), 0, stream, p);
-  QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
-  return QNN_OK;
+template <int BM, int BN, bool FUSED>
+static void launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
+  hipLaunchKernelGGL((qconv_kernel<BM, BN, FUSED>), dim3(nblk), dim3(256), 0, s, x, w, p);
 }
 
 }  // namespace qnn
 
 using namespace qnn;
 
-extern "C" int qnn_qconv2d_fwd(const int8_t* x, int n, int h, int w, int cp, const int8_t* wq, int cout, int cout_pad,
-                               int kh, int kw, int sh, int sw, int ph, int pw, int ho, int wo, const float* sxsw,
-                               const float* sxbw, const float* table, const int* hcls, const int* wcls, int nwc,
-                               const float* bias, float* y, int out_layout, qnn_stream_t stream) {
-  QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && cout > 0 && kh > 0 && kw > 0 && sh > 0 && sw > 0 && ph >= 0 && pw >= 0,
+extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
+                               qnn_stream_t stream) {
+  QNN_REQUIRE(desc && epi, "null descriptor");
+  const qnn_conv_desc& d = *desc;
+  const qnn_epilogue& e = *epi;
+  QNN_REQUIRE(d.n >= 0 && d.hp > 0 && d.wp > 0 && d.cout > 0 && d.kh > 0 && d.kw > 0 && d.sh > 0 && d.sw > 0,
               "bad shape");
-  QNN_REQUIRE(cp > 0 && cp % 16 == 0, "cp must be a positive multiple of 16");
-  QNN_REQUIRE(ho == (h + 2 * ph - kh) / sh + 1 && wo == (w + 2 * pw - kw) / sw + 1, "ho/wo inconsistent");
-  QNN_REQUIRE(out_layout == 0 || out_layout == 1, "out_layout must be 0 or 1");
-  QNN_REQUIRE(nwc > 0, "nwc must be > 0");
-  if (n == 0) return QNN_OK;
-  QNN_REQUIRE(x && wq && sxsw && sxbw && table && hcls && wcls && y, "null pointer");
+  QNN_REQUIRE(d.cp >= 16 && (d.cp & (d.cp - 1)) == 0, "cp must be 16 * 2^j");
+  QNN_REQUIRE(d.kh * d.kw <= MAX_TAPS, "at most 64 taps");
+  QNN_REQUIRE(d.ho > 0 && d.wo > 0 && (d.ho - 1) * d.sh + d.kh <= d.hp && (d.wo - 1) * d.sw + d.kw <= d.wp,
+              "ho/wo exceed the padded input");
+  QNN_REQUIRE(d.kpad % BK == 0 && d.kpad >= d.kh * d.kw * d.cp, "kpad must be a multiple of 128 covering K");
+  QNN_REQUIRE((int64_t)d.n * d.hp * d.wp * d.cp < (1LL << 31) && d.zero_off >= 0 && d.zero_off % 16 == 0,
+              "input too large or bad zero_off");
+  QNN_REQUIRE(e.nclass > 0 && e.nclass <= MAX_CLASSES && e.nwc > 0, "border classes out of range");
+  QNN_REQUIRE(e.mode == 0 || e.mode == 1, "mode must be 0 (drop-in NCHW) or 1 (fused NHWC)");
+  if (d.n == 0) return QNN_OK;
+  QNN_REQUIRE(x && wq && e.sxsw && e.sxbw && e.table && e.hcls && e.wcls, "null pointer");
   QNN_REQUIRE((((uintptr_t)x) & 15) == 0 && (((uintptr_t)wq) & 15) == 0, "x/wq must be 16-byte aligned");
-  ConvParams p;
-  p.x = x; p.w = wq; p.y = y; p.sxsw = sxsw; p.sxbw = sxbw; p.table = table; p.hcls = hcls; p.wcls = wcls;
-  p.bias = bias;
-  p.N = n; p.H = h; p.W = w; p.Cp = cp; p.Cout = cout; p.KH = kh; p.KW = kw; p.SH = sh; p.SW = sw; p.PH = ph; p.PW = pw;
-  p.Ho = ho; p.Wo = wo;
-  p.K = kh * kw * cp;
-  p.kpad = (int)(cdiv((int64_t)p.K, BK) * BK);
-  int64_t M = (int64_t)n * ho * wo;
+  if (e.mode == 0) {
+    QNN_REQUIRE(e.out_f32 != nullptr, "mode 0 needs out_f32");
+  } else {
+    QNN_REQUIRE(d.cout % 4 == 0, "fused mode needs cout % 4 == 0");
+    QNN_REQUIRE(!e.bn_mean || (e.bn_sq && e.bn_wq && e.bn_bq && e.bn_scale > 0.f), "incomplete RangeBN");
+    QNN_REQUIRE(!e.out_code0 || (e.code0_cp % 4 == 0 && e.code0_scale > 0.f), "bad code0");
+    QNN_REQUIRE(!e.out_code1 || (e.code1_cp % 4 == 0 && e.code1_scale > 0.f), "bad code1");
+    QNN_REQUIRE(e.out_f32 || e.out_code0 || e.out_code1 || e.out_bncode, "fused mode without an output");
+  }
+  Params p;
+  p.d = d;
+  p.e = e;
+  const int64_t M = (int64_t)d.n * d.ho * d.wo;
   QNN_REQUIRE(M < (1LL << 31), "too many output pixels");
   p.M = (int)M;
-  p.nwc = nwc;
-  p.out_layout = out_layout;
+  p.taps = d.kh * d.kw;
+  p.lgcpt = __builtin_ctz(d.cp / 16);
+  p.nstage = d.kpad / BK;
   hipStream_t s = (hipStream_t)stream;
-  // tile choice: 64-channel tiles for narrow layers, 128x128 otherwise
-  if (cout <= 64) {
-    QNN_REQUIRE(cout_pad >= 64 && cout_pad % 64 == 0, "cout_pad must be a multiple of 64 (>= 64)");
-    return launch<1, 4, 2, 2>(p, s);  // 64 x 256
+  const bool narrow = d.cout <= 64;
+  QNN_REQUIRE(d.cout_pad >= (narrow ? 64 : 128) * (int)cdiv(d.cout, narrow ? 64 : 128), "cout_pad too small");
+  if (e.mode == 0) {
+    if (narrow) launch<64, 256, false>(x, wq, p, s);
+    else launch<128, 128, false>(x, wq, p, s);
+  } else {
+    if (narrow) launch<64, 256, true>(x, wq, p, s);
+    else launch<128, 128, true>(x, wq, p, s);
   }
-  QNN_REQUIRE(cout_pad % 128 == 0, "cout_pad must be a multiple of 128 when cout > 64");
-  return launch<2, 2, 2, 2>(p, s);    // 128 x 128
+  QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
+  return QNN_OK;
 }

@@ -101,40 +101,75 @@ __global__ __launch_bounds__(1024) void fake_quant_vec_kernel(const float* __res
   for (int i = threadIdx.x; i < n; i += blockDim.x) y[i] = fake_quant(x[i], -mn, mn, s, qmax);
 }
 
-// ------------------------------------------------------------------ NCHW -> NHWC8
-// Each thread: one pixel, 16 channels (one 16-byte output chunk).  Reads are
-// coalesced along the pixel index, writes are 16 B per lane.
-__global__ void quantize_nchw_nhwc8_kernel(const float* __restrict__ x, int8_t* __restrict__ q, int n, int c,
-                                           int hw, int cp, float neg_min, float scale, float qmax) {
-  int64_t npix = (int64_t)n * hw;
-  int groups = cp >> 4;
-  int64_t total = npix * groups;
+// ------------------------------------------------------------------ NCHW -> padded NHWC8
+// One thread per (padded pixel, 16-channel group): interior pixels quantize 16
+// channels (reads coalesced along w), border pixels / pad channels write code' 0.
+__global__ void quantize_nchw_nhwc8_kernel(const float* __restrict__ x, int8_t* __restrict__ q, int n, int c, int h,
+                                           int w, int pad, int cp, float neg_min, float scale, float qmax) {
+  const int hp = h + 2 * pad, wp = w + 2 * pad, groups = cp >> 4;
+  const int64_t npix = (int64_t)n * hp * wp;
+  const int64_t total = npix * groups;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t pix = idx % npix;
-    int g = (int)(idx / npix);
-    int64_t img = pix / hw;
-    int64_t p = pix - img * hw;
-    const float* src = x + (img * c) * hw + p;
+    const int64_t pix = idx % npix;
+    const int g = (int)(idx / npix);
+    const int wq = (int)(pix % wp);
+    const int64_t t = pix / wp;
+    const int hq = (int)(t % hp);
+    const int64_t img = t / hp;
+    const int iy = hq - pad, ix = wq - pad;
     union {
       int8_t b[16];
       int4 v;
     } out;
+    out.v = make_int4(0, 0, 0, 0);
+    if (iy >= 0 && iy < h && ix >= 0 && ix < w) {
+      const float* src = x + (img * c) * (int64_t)h * w + (int64_t)iy * w + ix;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      int ch = g * 16 + j;
-      int8_t code = 0;
-      if (ch < c) code = (int8_t)((int)quant_code(src[(int64_t)ch * hw], neg_min, scale, qmax) - 128);
-      out.b[j] = code;
+      for (int j = 0; j < 16; ++j) {
+        const int ch = g * 16 + j;
+        if (ch < c) out.b[j] = (int8_t)((int)quant_code(src[(int64_t)ch * h * w], neg_min, scale, qmax) - 128);
+      }
     }
     *reinterpret_cast<int4*>(q + pix * cp + g * 16) = out.v;
   }
+  if (blockIdx.x == 0 && threadIdx.x < 8)  // 128-byte zero page after the tensor
+    *reinterpret_cast<int4*>(q + npix * cp + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
+}
+
+// Space-to-depth codes (factor 2): z[n][h2][w2][(2u+v)*c + ci], 16 channels.
+__global__ void quantize_s2d_kernel(const float* __restrict__ x, int8_t* __restrict__ z, int n, int c, int h, int w,
+                                    int pad, int hz, int wz, float neg_min, float scale, float qmax) {
+  const int64_t npix = (int64_t)n * hz * wz;
+  for (int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pix < npix;
+       pix += (int64_t)gridDim.x * blockDim.x) {
+    const int w2 = (int)(pix % wz);
+    const int64_t t = pix / wz;
+    const int h2 = (int)(t % hz);
+    const int64_t img = t / hz;
+    union {
+      int8_t b[16];
+      int4 v;
+    } out;
+    out.v = make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int uv = 0; uv < 4; ++uv) {
+      const int iy = 2 * h2 + (uv >> 1) - pad, ix = 2 * w2 + (uv & 1) - pad;
+      if (iy < 0 || iy >= h || ix < 0 || ix >= w) continue;
+      const float* src = x + (img * c) * (int64_t)h * w + (int64_t)iy * w + ix;
+      for (int ci = 0; ci < c; ++ci)
+        out.b[uv * c + ci] = (int8_t)((int)quant_code(src[(int64_t)ci * h * w], neg_min, scale, qmax) - 128);
+    }
+    *reinterpret_cast<int4*>(z + pix * 16) = out.v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 8)
+    *reinterpret_cast<int4*>(z + npix * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
 // ------------------------------------------------------------------ weight pack
 // One block per (padded) output channel.  Deterministic fp64 tap sums.
 __global__ __launch_bounds__(256) void pack_weight_kernel(const float* __restrict__ w, int cout, int cin_g, int kh,
-                                                          int kw, int cin_pad, int kpad, float qmax,
+                                                          int kw, int cin_pad, int kpad, int s2d, float qmax,
                                                           const float* w_min_in, const float* w_max_in,
                                                           int8_t* __restrict__ wq, float* s_w, float* b_w,
                                                           float* tap_sum, float* w_hat, float* w_min_out,
@@ -179,15 +214,25 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const float* __restric
     if (w_min_out) w_min_out[c] = mn;
     if (w_max_out) w_max_out[c] = mx;
   }
-  // packed row: [tap][cin_pad] codes, zero tail up to kpad
+  const int pkw = s2d ? (kw + 1) / 2 : kw;
+  const int ptaps = s2d ? ((kh + 1) / 2) * pkw : taps;
   for (int i = threadIdx.x; i < kpad; i += blockDim.x) {
     int8_t code = 0;
-    int tap = i / cin_pad;
-    int ci = i - tap * cin_pad;
-    if (tap < taps && ci < cin_g) {
-      float q = quant_code(wc[ci * taps + tap], neg_min, s, qmax);
-      code = (int8_t)((int)q - 128);
+    const int tap = i / cin_pad;
+    const int cc = i - tap * cin_pad;
+    int r = -1, sx = -1, ci = -1;
+    if (tap < ptaps) {
+      if (!s2d) {
+        if (cc < cin_g) { r = tap / kw; sx = tap - r * kw; ci = cc; }
+      } else if (cc < 4 * cin_g) {
+        const int uv = cc / cin_g, a = tap / pkw, b = tap - a * pkw;
+        ci = cc - uv * cin_g;
+        r = 2 * a + (uv >> 1);
+        sx = 2 * b + (uv & 1);
+        if (r >= kh || sx >= kw) r = -1;
+      }
     }
+    if (r >= 0) code = (int8_t)((int)quant_code(wc[ci * taps + r * kw + sx], neg_min, s, qmax) - 128);
     row[i] = code;
   }
   if (w_hat) {
@@ -352,30 +397,45 @@ int qnn_fake_quant_vec_f32(const float* x, float* y, int n, float qmax, int scal
   return QNN_OK;
 }
 
-int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, int w, int cp, float neg_min,
-                               float scale, float qmax, qnn_stream_t stream) {
-  QNN_REQUIRE(n >= 0 && c > 0 && h > 0 && w > 0, "bad shape");
+int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, int w, int pad, int cp,
+                               float neg_min, float scale, float qmax, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && c > 0 && h > 0 && w > 0 && pad >= 0, "bad shape");
   QNN_REQUIRE(cp >= c && cp % 16 == 0, "cp must be a multiple of 16 and >= c");
   QNN_REQUIRE(scale > 0.f, "scale must be > 0");
-  if (n == 0) return QNN_OK;
-  QNN_REQUIRE(x && q, "null pointer");
-  int64_t work = (int64_t)n * h * w * (cp / 16);
-  hipLaunchKernelGGL(quantize_nchw_nhwc8_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream, x, q,
-                     n, c, h * w, cp, neg_min, scale, qmax);
+  QNN_REQUIRE(q && (n == 0 || x), "null pointer");
+  QNN_REQUIRE((((uintptr_t)q) & 15) == 0, "q must be 16-byte aligned");
+  int64_t work = (int64_t)n * (h + 2 * pad) * (w + 2 * pad) * (cp / 16);
+  hipLaunchKernelGGL(quantize_nchw_nhwc8_kernel, dim3(grid_for(work > 0 ? work : 1, 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, q, n, c, h, w, pad, cp, neg_min, scale, qmax);
   QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_nhwc8");
   return QNN_OK;
 }
 
-int qnn_pack_weight_i8(const float* w, int cout, int cin_g, int kh, int kw, int cin_pad, int cout_pad, float qmax,
-                       const float* w_min_in, const float* w_max_in, int8_t* wq, float* s_w, float* b_w,
+int qnn_quantize_nchw_to_s2d8(const float* x, int8_t* z, int n, int c, int h, int w, int pad, int hz, int wz,
+                              float neg_min, float scale, float qmax, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && c > 0 && 4 * c <= 16 && h > 0 && w > 0 && pad >= 0 && hz > 0 && wz > 0, "bad shape");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  QNN_REQUIRE(z && (n == 0 || x), "null pointer");
+  QNN_REQUIRE((((uintptr_t)z) & 15) == 0, "z must be 16-byte aligned");
+  int64_t work = (int64_t)n * hz * wz;
+  hipLaunchKernelGGL(quantize_s2d_kernel, dim3(grid_for(work > 0 ? work : 1, 256)), dim3(256), 0, (hipStream_t)stream,
+                     x, z, n, c, h, w, pad, hz, wz, neg_min, scale, qmax);
+  QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_s2d8");
+  return QNN_OK;
+}
+
+int qnn_pack_weight_i8(const float* w, int cout, int cin_g, int kh, int kw, int cin_pad, int cout_pad, int s2d,
+                       float qmax, const float* w_min_in, const float* w_max_in, int8_t* wq, float* s_w, float* b_w,
                        float* tap_sum, float* w_hat, float* w_min_out, float* w_max_out, qnn_stream_t stream) {
   QNN_REQUIRE(cout > 0 && cin_g > 0 && kh > 0 && kw > 0, "bad shape");
-  QNN_REQUIRE(cin_pad >= cin_g && cout_pad >= cout, "padding smaller than shape");
+  QNN_REQUIRE(s2d == 0 || s2d == 2, "s2d must be 0 or 2");
+  QNN_REQUIRE(cin_pad >= (s2d ? 4 * cin_g : cin_g) && cout_pad >= cout, "padding smaller than shape");
   QNN_REQUIRE(w && wq && s_w && b_w, "null pointer");
   QNN_REQUIRE((w_min_in == nullptr) == (w_max_in == nullptr), "w_min_in/w_max_in must both be set or both null");
-  int kpad = (int)(cdiv((int64_t)kh * kw * cin_pad, 64) * 64);
+  const int64_t ptaps = s2d ? (int64_t)((kh + 1) / 2) * ((kw + 1) / 2) : (int64_t)kh * kw;
+  const int kpad = (int)(cdiv(ptaps * cin_pad, 128) * 128);
   hipLaunchKernelGGL(pack_weight_kernel, dim3(cout_pad), dim3(256), 0, (hipStream_t)stream, w, cout, cin_g, kh, kw,
-                     cin_pad, kpad, qmax, w_min_in, w_max_in, wq, s_w, b_w, tap_sum, w_hat, w_min_out, w_max_out);
+                     cin_pad, kpad, s2d, qmax, w_min_in, w_max_in, wq, s_w, b_w, tap_sum, w_hat, w_min_out, w_max_out);
   QNN_LAUNCH_CHECK("qnn_pack_weight_i8");
   return QNN_OK;
 }

@@ -16,21 +16,42 @@ import torch  # noqa: F401  (binds the process HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libqnn_hip.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+
+class ConvDesc(ctypes.Structure):
+    """qnn_conv_desc (include/qnn.h)."""
+    _fields_ = [(n, c_int) for n in ("n", "hp", "wp", "cp", "zero_off", "cout", "cout_pad", "kh", "kw", "sh", "sw",
+                                     "ho", "wo", "kpad")]
+
+
+class Epilogue(ctypes.Structure):
+    """qnn_epilogue (include/qnn.h)."""
+    _fields_ = [("mode", c_int), ("sxsw", c_ptr), ("sxbw", c_ptr), ("table", c_ptr), ("hcls", c_ptr),
+                ("wcls", c_ptr), ("nwc", c_int), ("nclass", c_int), ("bias", c_ptr),
+                ("bn_mean", c_ptr), ("bn_sq", c_ptr), ("bn_wq", c_ptr), ("bn_bq", c_ptr),
+                ("bn_neg_min", c_float), ("bn_min", c_float), ("bn_scale", c_float), ("bn_qmax", c_float),
+                ("residual", c_ptr), ("relu", c_int), ("out_f32", c_ptr), ("out_bncode", c_ptr),
+                ("out_code0", c_ptr), ("code0_cp", c_int), ("code0_pad", c_int), ("code0_hp", c_int),
+                ("code0_wp", c_int), ("code0_neg_min", c_float), ("code0_scale", c_float), ("code0_qmax", c_float),
+                ("out_code1", c_ptr), ("code1_cp", c_int), ("code1_pad", c_int), ("code1_hp", c_int),
+                ("code1_wp", c_int), ("code1_neg_min", c_float), ("code1_scale", c_float), ("code1_qmax", c_float)]
 
 # name -> argtypes (restype is int status for all but the two metadata calls)
 SIGNATURES = {
     "qnn_fake_quant_f32": [c_ptr, c_ptr, c_i64, c_float, c_float, c_float, c_float, c_ptr],
     "qnn_fake_quant_rows_f32": [c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_float, c_ptr],
     "qnn_fake_quant_vec_f32": [c_ptr, c_ptr, c_int, c_float, c_int, c_ptr, c_ptr],
-    "qnn_quantize_nchw_to_nhwc8": [c_ptr, c_ptr, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_ptr],
-    "qnn_pack_weight_i8": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_ptr, c_ptr, c_ptr, c_ptr,
-                           c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "qnn_quantize_nchw_to_nhwc8": [c_ptr, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                                   c_float, c_ptr],
+    "qnn_quantize_nchw_to_s2d8": [c_ptr, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                                  c_float, c_ptr],
+    "qnn_pack_weight_i8": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_ptr, c_ptr, c_ptr,
+                           c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_conv_border_table": [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_float, c_ptr, c_ptr],
-    "qnn_qconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                        c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_int, c_ptr],
+    "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
     "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,

@@ -26,6 +26,7 @@ Host-scalar caching: the reference reads `float(running_min)` on every call
 and epilogue vectors are cached and keyed on the tensors' version counters, so a
 steady-state eval forward issues no synchronisation.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -222,11 +223,13 @@ class QuantMeasure(nn.Module, QuantNode):
 # ============================================================ packed operands
 class _Packed:
     """Device-resident int8 operands of one QConv2d/QLinear weight version."""
-    __slots__ = ("key", "wq", "s_w", "b_w", "tap_sum", "w_hat", "qbias", "cin_pad", "cout_pad", "geom", "epi")
+    __slots__ = ("key", "wq", "s_w", "b_w", "tap_sum", "w_hat", "qbias", "cin_pad", "cout_pad", "kpad", "s2d",
+                 "ptaps", "geom", "epi")
 
 
-def _border_classes(size, k, stride, pad, out):
-    """Distinct [lo, hi) valid-tap ranges over output positions (zero padding)."""
+def border_classes(size, k, stride, pad, out):
+    """Distinct [lo, hi) valid-tap ranges over the output positions of one spatial
+    dim (zero padding): the classes of the border-aware zero-point table."""
     cls, ranges, ids = [], [], {}
     for o in range(out):
         lo = max(0, pad - o * stride)
@@ -239,6 +242,19 @@ def _border_classes(size, k, stride, pad, out):
     return cls, ranges
 
 
+def channel_pad(c):
+    """Cp = 16 * 2^j >= c (the kernel's K-chunk addressing needs a power of two)."""
+    cp = 16
+    while cp < c:
+        cp *= 2
+    return cp
+
+
+def use_s2d(cin_g, kh, stride):
+    """Space-to-depth for stride-2 stems on <= 4 channels (7x7/2, 3x3/2)."""
+    return tuple(stride) == (2, 2) and 4 * cin_g <= 16 and kh > 1
+
+
 class _QLayerMixin:
     """Shared int8 machinery of QConv2d / QLinear (QuantNode subclasses)."""
 
@@ -249,12 +265,12 @@ class _QLayerMixin:
         w = self.weight
         return w if w.dim() == 4 else w.view(w.shape[0], w.shape[1], 1, 1)
 
-    def _pack(self, depthwise=False):
+    def _pack(self, depthwise=False, s2d=False):
         w = self.weight
         bias = self.bias
         freeze = bool(self.freeze_param_dyn_range)
         key = (w.data_ptr(), w._version, None if bias is None else (bias.data_ptr(), bias._version), freeze,
-               self.num_bits_weight, self.bias_quant, depthwise, w.device)
+               self.num_bits_weight, self.bias_quant, depthwise, s2d, w.device)
         pk = self._qpack
         if pk is not None and pk.key == key:
             return pk
@@ -268,10 +284,16 @@ class _QLayerMixin:
         dev = w.device
         pk = _Packed()
         pk.key = key
-        pk.cin_pad = _round_up(cin_g, 16)
+        pk.s2d = s2d
+        if s2d:
+            pk.cin_pad = 16
+            pk.ptaps = ((kh + 1) // 2) * ((kw + 1) // 2)
+        else:
+            pk.cin_pad = channel_pad(cin_g)
+            pk.ptaps = kh * kw
         pk.cout_pad = _round_up(cout, 64) if cout <= 64 else _round_up(cout, 128)
-        kpad = _round_up(kh * kw * pk.cin_pad, 64)
-        pk.wq = torch.empty((pk.cout_pad, kpad), dtype=torch.int8, device=dev)
+        pk.kpad = _round_up(pk.ptaps * pk.cin_pad, 128)
+        pk.wq = torch.empty((pk.cout_pad, pk.kpad), dtype=torch.int8, device=dev)
         pk.s_w = torch.empty(cout, dtype=torch.float32, device=dev)
         pk.b_w = torch.empty(cout, dtype=torch.float32, device=dev)
         pk.tap_sum = torch.empty((cout, kh * kw), dtype=torch.float32, device=dev)
@@ -286,8 +308,8 @@ class _QLayerMixin:
             # weight_min/max buffers are rewritten every forward (quantize.py:317-323)
             wmin_out = torch.empty(cout, dtype=torch.float32, device=dev)
             wmax_out = torch.empty(cout, dtype=torch.float32, device=dev)
-        _lib.call("qnn_pack_weight_i8", _lib.ptr(w4), cout, cin_g, kh, kw, pk.cin_pad, pk.cout_pad, qmax,
-                  _lib.ptr(wmin_in), _lib.ptr(wmax_in), _lib.ptr(pk.wq), _lib.ptr(pk.s_w), _lib.ptr(pk.b_w),
+        _lib.call("qnn_pack_weight_i8", _lib.ptr(w4), cout, cin_g, kh, kw, pk.cin_pad, pk.cout_pad, 2 if s2d else 0,
+                  qmax, _lib.ptr(wmin_in), _lib.ptr(wmax_in), _lib.ptr(pk.wq), _lib.ptr(pk.s_w), _lib.ptr(pk.b_w),
                   _lib.ptr(pk.tap_sum), _lib.ptr(pk.w_hat), _lib.ptr(wmin_out), _lib.ptr(wmax_out), st)
         if not freeze:
             self.weight_min = wmin_out.view(self.scale_shape)
@@ -313,18 +335,22 @@ class _QLayerMixin:
         self._qpack = pk
         return pk
 
-    def _geometry(self, pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev):
+    @staticmethod
+    def _geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev):
         gk = (H, W)
         g = pk.geom.get(gk)
         if g is None:
-            hc, hr = _border_classes(H, kh, sh, ph, Ho)
-            wc, wr = _border_classes(W, kw, sw, pw, Wo)
+            hc, hr = border_classes(H, kh, sh, ph, Ho)
+            wc, wr = border_classes(W, kw, sw, pw, Wo)
+            if len(hr) * len(wr) > 64:
+                raise NotImplementedError("qnn: more than 64 border classes")
             t = lambda a: torch.tensor(np.asarray(a, dtype=np.int32).reshape(-1), device=dev)
             g = (t(hc), t(hr), len(hr), t(wc), t(wr), len(wr))
             pk.geom[gk] = g
         return g
 
-    def _epilogue(self, pk, g, gk, s_x, b_x, kh, kw):
+    @staticmethod
+    def _epilogue(pk, g, gk, s_x, b_x, kh, kw):
         ek = (gk, s_x, b_x)
         e = pk.epi.get(ek)
         if e is None:
@@ -341,9 +367,9 @@ class _QLayerMixin:
             pk.epi[ek] = e
         return e
 
-    def _int8_forward(self, x4, rng, stride, padding, out_layout=0):
-        """Quantize x (NCHW fp32) to NHWC8 codes and run the MFMA conv."""
-        pk = self._pack()
+    def _int8_forward(self, x4, rng, stride, padding):
+        """Quantize x (NCHW fp32) into the padded (or space-to-depth) NHWC8 layout and
+        run the MFMA conv in drop-in mode (fp32 NCHW out)."""
         w4 = self._weight4()
         cout, cin_g, kh, kw = w4.shape
         N, C, H, W = x4.shape
@@ -351,6 +377,10 @@ class _QLayerMixin:
             raise RuntimeError(f"qnn: expected {cin_g} input channels, got {C}")
         sh, sw = stride
         ph, pw = padding
+        if ph != pw:
+            raise NotImplementedError("qnn: asymmetric padding is not on the int8 path")
+        s2d = use_s2d(cin_g, kh, stride)
+        pk = self._pack(s2d=s2d)
         Ho = (H + 2 * ph - kh) // sh + 1
         Wo = (W + 2 * pw - kw) // sw + 1
         if Ho <= 0 or Wo <= 0:
@@ -362,18 +392,34 @@ class _QLayerMixin:
         b_x = 128.0 * s32 + float(np.float32(mn))
         dev = x4.device
         st = _lib.stream_of(x4)
-        xq = torch.empty((N, H, W, pk.cin_pad), dtype=torch.int8, device=dev)
-        _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, pk.cin_pad, -float(mn), s,
-                  qmax, st)
+        d = _lib.ConvDesc()
+        d.n, d.cout, d.cout_pad, d.ho, d.wo, d.kpad = N, cout, pk.cout_pad, Ho, Wo, pk.kpad
+        if s2d:
+            d.kh, d.kw, d.sh, d.sw, d.cp = (kh + 1) // 2, (kw + 1) // 2, 1, 1, 16
+            d.hp, d.wp = Ho - 1 + d.kh, Wo - 1 + d.kw
+            nbytes = N * d.hp * d.wp * 16
+            xq = torch.empty(nbytes + 128, dtype=torch.int8, device=dev)
+            _lib.call("qnn_quantize_nchw_to_s2d8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, ph, d.hp, d.wp, -float(mn),
+                      s, qmax, st)
+        else:
+            d.kh, d.kw, d.sh, d.sw, d.cp = kh, kw, sh, sw, pk.cin_pad
+            d.hp, d.wp = H + 2 * ph, W + 2 * pw
+            nbytes = N * d.hp * d.wp * d.cp
+            xq = torch.empty(nbytes + 128, dtype=torch.int8, device=dev)
+            _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, ph, d.cp, -float(mn), s,
+                      qmax, st)
+        d.zero_off = nbytes
         g = self._geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev)
         sxsw, sxbw, table = self._epilogue(pk, g, (H, W), s32, b_x, kh, kw)
-        if out_layout == 0:
-            y = torch.empty((N, cout, Ho, Wo), dtype=torch.float32, device=dev)
-        else:
-            y = torch.empty((N, Ho, Wo, cout), dtype=torch.float32, device=dev)
-        _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), N, H, W, pk.cin_pad, _lib.ptr(pk.wq), cout, pk.cout_pad, kh, kw,
-                  sh, sw, ph, pw, Ho, Wo, _lib.ptr(sxsw), _lib.ptr(sxbw), _lib.ptr(table), _lib.ptr(g[0]), _lib.ptr(g[3]),
-                  g[5], _lib.ptr(pk.qbias), _lib.ptr(y), out_layout, st)
+        y = torch.empty((N, cout, Ho, Wo), dtype=torch.float32, device=dev)
+        e = _lib.Epilogue()
+        e.mode = 0
+        e.sxsw, e.sxbw, e.table, e.hcls, e.wcls = (sxsw.data_ptr(), sxbw.data_ptr(), table.data_ptr(),
+                                                   g[0].data_ptr(), g[3].data_ptr())
+        e.nwc, e.nclass = g[5], g[2] * g[5]
+        e.bias = None if pk.qbias is None else pk.qbias.data_ptr()
+        e.out_f32 = y.data_ptr()
+        _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
         return y
 
 

@@ -50,24 +50,51 @@ def test_bindings_cover_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.qnn_abi_version() == 1
+    assert lib.qnn_abi_version() == 2
 
 
 def test_argument_validation_without_device(lib):
+    import ctypes
+    from qnn import _lib
     # invalid arguments are rejected before any HIP call, with a message
     rc = lib.qnn_fake_quant_f32(None, None, 16, 0.0, 0.0, 0.0, 255.0, None)
     assert rc == 1
     assert b"scale" in lib.qnn_last_error() or b"null" in lib.qnn_last_error()
-    rc = lib.qnn_qconv2d_fwd(None, 1, 8, 8, 17, None, 64, 64, 3, 3, 1, 1, 1, 1, 8, 8, None, None, None, None, None, 1,
-                             None, None, 0, None)
+    d = _lib.ConvDesc(n=1, hp=10, wp=10, cp=24, zero_off=0, cout=64, cout_pad=64, kh=3, kw=3, sh=1, sw=1, ho=8, wo=8,
+                      kpad=256)
+    e = _lib.Epilogue(mode=0, nwc=1, nclass=1)
+    rc = lib.qnn_qconv2d_fwd(None, None, ctypes.byref(d), ctypes.byref(e), None)
     assert rc == 1 and b"cp" in lib.qnn_last_error()
-    rc = lib.qnn_qconv2d_fwd(None, 1, 8, 8, 16, None, 64, 64, 3, 3, 1, 1, 1, 1, 7, 8, None, None, None, None, None, 1,
-                             None, None, 0, None)
+    d.cp, d.ho = 16, 9
+    rc = lib.qnn_qconv2d_fwd(None, None, ctypes.byref(d), ctypes.byref(e), None)
     assert rc == 1 and b"ho/wo" in lib.qnn_last_error()
+    d.ho, d.kpad = 8, 100
+    rc = lib.qnn_qconv2d_fwd(None, None, ctypes.byref(d), ctypes.byref(e), None)
+    assert rc == 1 and b"kpad" in lib.qnn_last_error()
     rc = lib.qnn_fake_quant_vec_f32(None, None, 70000, 255.0, 0, None, None)
     assert rc == 1
+    rc = lib.qnn_quantize_nchw_to_s2d8(None, None, 1, 5, 8, 8, 1, 5, 5, 0.0, 1.0, 255.0, None)
+    assert rc == 1  # 4*c > 16
     # empty batches are a no-op success
     assert lib.qnn_fake_quant_f32(None, None, 0, 0.0, 0.0, 1.0, 255.0, None) == 0
+
+
+def test_struct_layout_matches_header():
+    """ctypes mirrors of qnn_conv_desc / qnn_epilogue have the C field order."""
+    import re as _re
+    from qnn import _lib
+    src = open(HEADER).read()
+    for cname, py in (("qnn_conv_desc", _lib.ConvDesc), ("qnn_epilogue", _lib.Epilogue)):
+        body = _re.search(r"typedef struct " + cname + r" \{(.*?)\} " + cname, src, _re.S).group(1)
+        body = _re.sub(r"/\*.*?\*/", "", body, flags=_re.S)
+        names = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            decl = _re.sub(r"^(const\s+)?\w+\s*\*?\s*", "", decl)
+            names += [n.strip().lstrip("*") for n in decl.split(",")]
+        assert names == [f[0] for f in py._fields_], cname
 
 
 def test_error_is_thread_local(lib):

@@ -69,41 +69,80 @@ def test_fake_quant_tensor_and_none_kat(gpu):
         j += 1
 
 
-@pytest.mark.parametrize("shape,c_pad", [((3, 24, 9, 11), 32), ((2, 3, 33, 17), 16), ((4, 64, 56, 56), 64)])
-def test_activation_codes_nhwc8(gpu, shape, c_pad):
+@pytest.mark.parametrize("shape,c_pad,pad", [((3, 24, 9, 11), 32, 1), ((2, 3, 33, 17), 16, 3), ((4, 64, 56, 56), 64, 0)])
+def test_activation_codes_padded_nhwc8(gpu, shape, c_pad, pad):
+    N, C, H, W = shape
     x = synthetic.input_batch(shape, 5) * 2.0
     mn, mx = -1.5, 3.25
-    q = torch.empty((shape[0], shape[2], shape[3], c_pad), dtype=torch.int8, device=gpu)
+    hp, wp = H + 2 * pad, W + 2 * pad
+    nbytes = N * hp * wp * c_pad
+    q = torch.full((nbytes + 128,), 77, dtype=torch.int8, device=gpu)  # poisoned
     s = max((mx - mn) / 255.0, 1e-8)
     xd = x.to(gpu)
-    _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(xd), _lib.ptr(q), shape[0], shape[1], shape[2], shape[3], c_pad,
-              -mn, s, 255.0, _lib.stream_of(xd))
+    _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(xd), _lib.ptr(q), N, C, H, W, pad, c_pad, -mn, s, 255.0,
+              _lib.stream_of(xd))
+    got = q[:nbytes].cpu().numpy().astype(np.int32).reshape(N, hp, wp, c_pad)
     ref = O.quantize_codes_np(x.numpy(), mn, mx).astype(np.int32) - 128  # N C H W
-    got = q.cpu().numpy().astype(np.int32)
-    np.testing.assert_array_equal(got[..., : shape[1]], ref.transpose(0, 2, 3, 1))
-    assert np.all(got[..., shape[1]:] == 0)
+    np.testing.assert_array_equal(got[:, pad:pad + H, pad:pad + W, :C], ref.transpose(0, 2, 3, 1))
+    inner = np.zeros((N, hp, wp, c_pad), dtype=bool)
+    inner[:, pad:pad + H, pad:pad + W, :C] = True
+    assert np.all(got[~inner] == 0)                              # border + channel pad = code' 0
+    assert np.all(q[nbytes:].cpu().numpy() == 0)                 # zero page
 
 
-@pytest.mark.parametrize("shape", [(64, 64, 3, 3), (40, 24, 3, 3), (64, 3, 7, 7), (1000, 512, 1, 1)])
-def test_weight_pack_bitexact(gpu, shape):
+def test_activation_codes_space_to_depth(gpu):
+    N, C, H, W, pad = 2, 3, 37, 30, 3
+    x = synthetic.input_batch((N, C, H, W), 6)
+    mn, mx = -2.0, 2.5
+    hz, wz = 21, 18
+    z = torch.full((N * hz * wz * 16 + 128,), 55, dtype=torch.int8, device=gpu)
+    xd = x.to(gpu)
+    _lib.call("qnn_quantize_nchw_to_s2d8", _lib.ptr(xd), _lib.ptr(z), N, C, H, W, pad, hz, wz, -mn,
+              max((mx - mn) / 255.0, 1e-8), 255.0, _lib.stream_of(xd))
+    got = z[: N * hz * wz * 16].cpu().numpy().astype(np.int32).reshape(N, hz, wz, 16)
+    codes = O.quantize_codes_np(x.numpy(), mn, mx).astype(np.int32) - 128
+    ref = np.zeros_like(got)
+    for h2 in range(hz):
+        for w2 in range(wz):
+            for u in range(2):
+                for v in range(2):
+                    iy, ix = 2 * h2 + u - pad, 2 * w2 + v - pad
+                    if 0 <= iy < H and 0 <= ix < W:
+                        ref[:, h2, w2, (2 * u + v) * C:(2 * u + v + 1) * C] = codes[:, :, iy, ix]
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("shape,s2d", [((64, 64, 3, 3), 0), ((40, 24, 3, 3), 0), ((64, 3, 7, 7), 0),
+                                       ((1000, 512, 1, 1), 0), ((64, 3, 7, 7), 2), ((32, 3, 3, 3), 2)])
+def test_weight_pack_bitexact(gpu, shape, s2d):
     w = torch.from_numpy(synthetic.normal(shape, 9, 0, 0.05))
     w[1] = 0.25  # constant channel -> scale floor
     cout, cin, kh, kw = shape
-    cin_pad = (cin + 15) // 16 * 16
+    cin_pad = 16 if s2d else max(16, 1 << (cin - 1).bit_length())
+    pkh, pkw = ((kh + 1) // 2, (kw + 1) // 2) if s2d else (kh, kw)
     cout_pad = (cout + 127) // 128 * 128
-    kpad = (kh * kw * cin_pad + 63) // 64 * 64
+    kpad = (pkh * pkw * cin_pad + 127) // 128 * 128
     wd = w.to(gpu)
-    wq = torch.empty((cout_pad, kpad), dtype=torch.int8, device=gpu)
+    wq = torch.full((cout_pad, kpad), 99, dtype=torch.int8, device=gpu)
     f = lambda *s: torch.empty(s, dtype=torch.float32, device=gpu)
     s_w, b_w, tap, what, wmin, wmax = f(cout), f(cout), f(cout, kh * kw), f(cout, cin * kh * kw), f(cout), f(cout)
-    _lib.call("qnn_pack_weight_i8", _lib.ptr(wd), cout, cin, kh, kw, cin_pad, cout_pad, 255.0, None, None,
+    _lib.call("qnn_pack_weight_i8", _lib.ptr(wd), cout, cin, kh, kw, cin_pad, cout_pad, s2d, 255.0, None, None,
               _lib.ptr(wq), _lib.ptr(s_w), _lib.ptr(b_w), _lib.ptr(tap), _lib.ptr(what), _lib.ptr(wmin),
               _lib.ptr(wmax), _lib.stream_of(wd))
     lo, hi = O.weight_ranges(w)
-    codes = O.codes_tensor_range(w, lo, hi).to(torch.int32) - 128            # [cout][cin][kh][kw]
-    packed = wq.cpu().to(torch.int32)[:cout, : kh * kw * cin_pad].view(cout, kh, kw, cin_pad)
-    assert torch.equal(packed[..., :cin], codes.permute(0, 2, 3, 1))
-    assert int(packed[..., cin:].abs().sum()) == 0 and int(wq.cpu()[cout:].abs().sum()) == 0
+    codes = (O.codes_tensor_range(w, lo, hi).to(torch.int32) - 128).numpy()      # [cout][cin][kh][kw]
+    packed = wq.cpu().numpy().astype(np.int32)
+    ref = np.zeros_like(packed)
+    for r in range(kh):
+        for sx in range(kw):
+            for ci in range(cin):
+                if s2d:
+                    a, u, b, v = r // 2, r % 2, sx // 2, sx % 2
+                    col = (a * pkw + b) * cin_pad + (2 * u + v) * cin + ci
+                else:
+                    col = (r * kw + sx) * cin_pad + ci
+                ref[:cout, col] = codes[:, ci, r, sx]
+    np.testing.assert_array_equal(packed, ref)
     w_hat = O.uniform_quantize(w, 8, lo, hi)
     np.testing.assert_array_equal(what.cpu().numpy(), w_hat.reshape(cout, -1).numpy())
     np.testing.assert_array_equal(wmin.cpu().numpy(), lo.reshape(-1).numpy())
