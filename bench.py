@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-iters", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--module-path", type=int, default=1, help="also time the per-module drop-in path (N=1)")
     args = ap.parse_args()
 
     from qnn import _lib
@@ -132,11 +133,13 @@ def main():
     model = build(device, args.depth)
     total_ops, mfma_ops = model_ops(model, args.batch)
     from qnn import synthetic
-    x = synthetic.input_batch((args.batch, 3, 224, 224), 1234 + rank).to(device)
-    runner = qdist.ShardedInference(model, args.batch * world)
+    from qnn.engine import Engine
+    engine = Engine(model, batch=args.batch)
+    engine.input.copy_(synthetic.input_batch((args.batch, 3, 224, 224), 1234 + rank).to(device))
+    runner = qdist.ShardedInference(engine, args.batch * world)
 
     def step():
-        return runner(x)
+        return runner(engine.input)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -147,7 +150,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = step()
+            step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -158,17 +161,35 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # Per-launch HIP-event timing of the MFMA conv kernel over a few extra forwards
-    timer = _lib.LaunchTimer(["qnn_qconv2d_fwd"])
+    # Per-launch HIP-event timing of every kernel of one forward (eager pass over the
+    # same launch sequence the graph replays; events on the launch stream)
+    names = sorted(set(engine.launch_names))
+    timer = _lib.LaunchTimer(names)
     _lib.set_timer(timer)
     reps = 3
     with torch.no_grad():
         for _ in range(reps):
-            model(x)
+            engine._run_ops()
     _lib.set_timer(None)
     d = timer.durations_ms()
-    conv_ms_per_fwd = sum(ms for _, ms in d) / reps
-    launches = len(d) // reps
+    per_kernel = {}
+    for n, ms in d:
+        per_kernel[n] = per_kernel.get(n, 0.0) + ms / reps
+    conv_ms_per_fwd = per_kernel.get("qnn_qconv2d_fwd", 0.0)
+    launches = engine.num_launches
+
+    module_ips = None
+    if args.module_path and world == 1:
+        with torch.no_grad():
+            x = engine.input.clone()
+            for _ in range(2):
+                model(x)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(max(2, args.steps // 4)):
+                model(x)
+            torch.cuda.synchronize()
+            module_ips = args.batch * max(2, args.steps // 4) / (time.perf_counter() - t1)
 
     if rank == 0:
         images = args.batch * world * args.steps
@@ -187,14 +208,18 @@ def main():
             "vs_baseline": None,
             "dtype": "int8",
             "data": "synthetic (N(0,1) 3x224x224 on device; numpy-PCG64 weights, reference init law)",
-            "config": {"workload": f"resnet_quantized depth={args.depth} imagenet eval forward, int8 MFMA path",
+            "config": {"workload": f"resnet_quantized depth={args.depth} imagenet eval forward, fused int8 engine "
+                                   f"(hipGraph), per-GPU batch {args.batch}",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "model_gop_per_batch": round(total_ops / 1e9, 2)},
-            "roofline": {"bound": "mfma", "kernel": "qconv_mfma_kernel (all QConv2d/QLinear launches of one forward)",
+            "roofline": {"bound": "mfma", "kernel": "qconv_kernel (all 21 QConv2d/QLinear launches of one forward)",
                          "achieved": round(achieved, 2), "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_INT8_TOPS, 4), "traffic": None,
-                         "launches_per_forward": launches, "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
+                         "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
                          "model_frac": round(total_ops / (ms_per_step * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4)},
+            "engine": {"launches_per_forward": launches, "hipgraph": True,
+                       "kernel_ms_per_forward": {k: round(v, 4) for k, v in per_kernel.items()}},
+            "module_path_images_per_s": None if module_ips is None else round(module_ips, 1),
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:

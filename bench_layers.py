@@ -51,7 +51,7 @@ def run(name, cfg, reps, dev):
         for _ in range(3):
             wrap(x)
         torch.cuda.synchronize()
-        timer = _lib.LaunchTimer(["qnn_qconv2d_fwd", "qnn_quantize_nchw_to_nhwc8"])
+        timer = _lib.LaunchTimer(["qnn_qconv2d_fwd", "qnn_quantize_nchw_to_nhwc8", "qnn_quantize_nchw_to_s2d8"])
         _lib.set_timer(timer)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

@@ -121,6 +121,10 @@ typedef struct qnn_conv_desc {
   int kh, kw, sh, sw;  /* taps and strides in the padded input's coordinates               */
   int ho, wo;          /* output pixel (ho, wo) reads input rows ho*sh + r, cols wo*sw + s */
   int kpad;            /* packed weight row stride in bytes (multiple of 128)              */
+  const int8_t* kmask; /* nullable: [kpad] 0/1 per K byte, 1 where the packed weights hold a
+                          real (tap, channel); sum_valid(q'_x) then counts only those bytes.
+                          Needed by space-to-depth stems (their 2x2-tap grid over-covers the
+                          kernel); NULL = every byte counts (codes past K are 0).  kpad <= 1024 */
 } qnn_conv_desc;
 
 /* Epilogue of the contraction.  Always:
@@ -187,6 +191,54 @@ int qnn_dwconv2d_fwd(const float* x, int n, int c, int h, int w, const float* w_
 int qnn_rangebn_f32(const float* x, float* y, int n, int c, int hw, float neg_min, float min, float scale,
                     float qmax, const float* mean, const float* sq, const float* wq, const float* bq,
                     const float* residual, int relu, qnn_stream_t stream);
+
+/* ---------------------------------------------------------------- fused model graph */
+
+/* RangeBN eval parameters (quantize.py:461-499) for the fused kernels below. */
+typedef struct qnn_bn_params {
+  const float* mean;  /* running_mean [c]                        */
+  const float* sq;    /* fake-quantized running_var [c]          */
+  const float* wq;    /* fake-quantized weight [c]               */
+  const float* bq;    /* fake-quantized bias [c]                 */
+  float neg_min, min, scale, qmax;  /* RangeBN.quantize_input range */
+} qnn_bn_params;
+
+/* Where and how to write requantized codes for a consumer conv: its QuantMeasure range
+ * and its padded NHWC8 input buffer [n][hp][wp][cp] (value at (h + pad, w + pad)). */
+typedef struct qnn_code_out {
+  int8_t* ptr;
+  int cp, pad, hp, wp;
+  float neg_min, scale, qmax;
+} qnn_code_out;
+
+/* ResNet stem max-pool (nn.MaxPool2d(3, 2, 1), resnet_quantized.py:174) fused with the
+ * ReLU and RangeBN before it (:140-143), on RangeBN's input codes q [n][h][w][c] (uint8,
+ * written by the stem conv's epilogue as out_bncode).  With
+ *   f_c(q) = fl(fl(fl(dequant(q) - mean) * sq) * wq) + bq,  g = relu o f_c,
+ * g is monotone per channel (direction sign(sq*wq)), so max over the window of
+ * g(q_i) = g(max q_i) (or g(min q_i)) exactly; padding positions are skipped (-inf).
+ * Outputs: out_f32 NHWC [n][ho][wo][c] (nullable) and codes for up to two consumers. */
+int qnn_maxpool_bncode(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
+                       const qnn_bn_params* bn, int relu, float* out_f32, const qnn_code_out* code0,
+                       const qnn_code_out* code1, qnn_stream_t stream);
+
+/* Depthwise QConv2d (groups == c, mobilenet_quantized.py:38-40) fused with its RangeBN and
+ * ReLU (:41-42) on padded NHWC8 codes x [n][hp][wp][cp] whose image interior is
+ * [pad, pad+h) x [pad, pad+w); taps outside it are skipped (zero padding of x_hat):
+ *   y = sum_taps x_hat * w_hat + bias, x_hat = fl(fl((q'+128) * x_scale) + x_min)  (the
+ *   reference's fake-quantized input values exactly), w_hat_t [kh*kw][c], bias = q(bias);
+ *   v = bn ? RangeBN_eval(y) : y;  v = relu ? max(v, 0) : v
+ * Outputs: out_f32 NHWC [n][ho][wo][c] (nullable), codes for one consumer (nullable). */
+int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                     const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min, float x_scale,
+                     const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
+                     const qnn_code_out* code0, qnn_stream_t stream);
+
+/* nn.AvgPool2d(k) over the whole k x k map (resnet_quantized.py:153, mobilenet_quantized.py:157)
+ * on NHWC fp32 x [n][hw][c]: mean = (sum in row-major tap order) / hw; writes out_f32 [n][c]
+ * (nullable) and the codes of the classifier's QuantMeasure into code0 (hp = wp = 1). */
+int qnn_avgpool_quant(const float* x, int n, int hw, int c, float* out_f32, const qnn_code_out* code0,
+                      qnn_stream_t stream);
 
 #ifdef __cplusplus
 }

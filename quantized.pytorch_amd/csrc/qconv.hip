@@ -33,6 +33,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int BK = 128;         // bytes of K per LDS stage (4 MFMA k-steps of 32)
 constexpr int MAX_TAPS = 64;
 constexpr int MAX_CLASSES = 64;
+constexpr int MAX_MASK = 1024;
 
 struct Params {
   qnn_conv_desc d;
@@ -59,7 +60,7 @@ __device__ __forceinline__ void store_code4(int8_t* p, float4 v, float nm, float
   *reinterpret_cast<int*>(p) = (b0 & 255) | ((b1 & 255) << 8) | ((b2 & 255) << 16) | ((b3 & 255) << 24);
 }
 
-template <int BM, int BN, bool FUSED>
+template <int BM, int BN, bool FUSED, bool MASKED>
 __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                     const Params p) {
   constexpr int WM = BM / 64, WN = BN / 64;
@@ -68,8 +69,9 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
   constexpr int NB = BN / 32;
   constexpr int STAGE = (BM + BN) * BK;
   // one LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) int8_t smem[2 * STAGE + 4 * MAX_TAPS];
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * STAGE + 4 * MAX_TAPS + (MASKED ? MAX_MASK : 0)];
   int* s_tap = reinterpret_cast<int*>(smem + 2 * STAGE);
+  int8_t* s_mask = smem + 2 * STAGE + 4 * MAX_TAPS;
 
   const qnn_conv_desc& d = p.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -90,6 +92,10 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
   const int HoWo = d.ho * d.wo;
 
   if (tid < p.taps) s_tap[tid] = ((tid / d.kw) * d.wp + (tid % d.kw)) * d.cp;
+  if constexpr (MASKED) {
+    for (int i = tid; i < d.kpad / 16; i += 256)
+      *reinterpret_cast<v4i*>(s_mask + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
+  }
 
   // ---- per-lane load state
   uint32_t boff[NB];
@@ -159,10 +165,12 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         fb[j] = *reinterpret_cast<const v4i*>(sb + swz(wn * 64 + j * 32 + frow, chunk));
-        int s = __builtin_amdgcn_sdot4(fb[j].x, 0x01010101, sumq[j], false);
-        s = __builtin_amdgcn_sdot4(fb[j].y, 0x01010101, s, false);
-        s = __builtin_amdgcn_sdot4(fb[j].z, 0x01010101, s, false);
-        sumq[j] = __builtin_amdgcn_sdot4(fb[j].w, 0x01010101, s, false);
+        v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
+        if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(s_mask + st * BK + 16 * chunk);
+        int s = __builtin_amdgcn_sdot4(fb[j].x, ones.x, sumq[j], false);
+        s = __builtin_amdgcn_sdot4(fb[j].y, ones.y, s, false);
+        s = __builtin_amdgcn_sdot4(fb[j].z, ones.z, s, false);
+        sumq[j] = __builtin_amdgcn_sdot4(fb[j].w, ones.w, s, false);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -267,7 +275,10 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
 template <int BM, int BN, bool FUSED>
 static void launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
-  hipLaunchKernelGGL((qconv_kernel<BM, BN, FUSED>), dim3(nblk), dim3(256), 0, s, x, w, p);
+  if (p.d.kmask)
+    hipLaunchKernelGGL((qconv_kernel<BM, BN, FUSED, true>), dim3(nblk), dim3(256), 0, s, x, w, p);
+  else
+    hipLaunchKernelGGL((qconv_kernel<BM, BN, FUSED, false>), dim3(nblk), dim3(256), 0, s, x, w, p);
 }
 
 }  // namespace qnn
@@ -288,6 +299,7 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   QNN_REQUIRE(d.kpad % BK == 0 && d.kpad >= d.kh * d.kw * d.cp, "kpad must be a multiple of 128 covering K");
   QNN_REQUIRE((int64_t)d.n * d.hp * d.wp * d.cp < (1LL << 31) && d.zero_off >= 0 && d.zero_off % 16 == 0,
               "input too large or bad zero_off");
+  QNN_REQUIRE(!d.kmask || (d.kpad <= MAX_MASK && (((uintptr_t)d.kmask) & 15) == 0), "kmask: kpad <= 1024, 16-B aligned");
   QNN_REQUIRE(e.nclass > 0 && e.nclass <= MAX_CLASSES && e.nwc > 0, "border classes out of range");
   QNN_REQUIRE(e.mode == 0 || e.mode == 1, "mode must be 0 (drop-in NCHW) or 1 (fused NHWC)");
   if (d.n == 0) return QNN_OK;

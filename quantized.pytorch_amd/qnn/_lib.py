@@ -24,7 +24,7 @@ c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, cty
 class ConvDesc(ctypes.Structure):
     """qnn_conv_desc (include/qnn.h)."""
     _fields_ = [(n, c_int) for n in ("n", "hp", "wp", "cp", "zero_off", "cout", "cout_pad", "kh", "kw", "sh", "sw",
-                                     "ho", "wo", "kpad")]
+                                     "ho", "wo", "kpad")] + [("kmask", c_ptr)]
 
 
 class Epilogue(ctypes.Structure):
@@ -38,6 +38,20 @@ class Epilogue(ctypes.Structure):
                 ("code0_wp", c_int), ("code0_neg_min", c_float), ("code0_scale", c_float), ("code0_qmax", c_float),
                 ("out_code1", c_ptr), ("code1_cp", c_int), ("code1_pad", c_int), ("code1_hp", c_int),
                 ("code1_wp", c_int), ("code1_neg_min", c_float), ("code1_scale", c_float), ("code1_qmax", c_float)]
+
+class BnParams(ctypes.Structure):
+    """qnn_bn_params (include/qnn.h)."""
+    _fields_ = [("mean", c_ptr), ("sq", c_ptr), ("wq", c_ptr), ("bq", c_ptr), ("neg_min", c_float),
+                ("min", c_float), ("scale", c_float), ("qmax", c_float)]
+
+
+class CodeOut(ctypes.Structure):
+    """qnn_code_out (include/qnn.h)."""
+    _fields_ = [("ptr", c_ptr), ("cp", c_int), ("pad", c_int), ("hp", c_int), ("wp", c_int), ("neg_min", c_float),
+                ("scale", c_float), ("qmax", c_float)]
+
+
+_PB, _PC = ctypes.POINTER(BnParams), ctypes.POINTER(CodeOut)
 
 # name -> argtypes (restype is int status for all but the two metadata calls)
 SIGNATURES = {
@@ -54,6 +68,11 @@ SIGNATURES = {
     "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
+    "qnn_maxpool_bncode": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,
+                           _PC, _PC, c_ptr],
+    "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
+                         c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
+    "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr, c_int, c_ptr],
 }

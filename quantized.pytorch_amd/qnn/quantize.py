@@ -224,7 +224,7 @@ class QuantMeasure(nn.Module, QuantNode):
 class _Packed:
     """Device-resident int8 operands of one QConv2d/QLinear weight version."""
     __slots__ = ("key", "wq", "s_w", "b_w", "tap_sum", "w_hat", "qbias", "cin_pad", "cout_pad", "kpad", "s2d",
-                 "ptaps", "geom", "epi")
+                 "ptaps", "kmask", "geom", "epi")
 
 
 def border_classes(size, k, stride, pad, out):
@@ -253,6 +253,21 @@ def channel_pad(c):
 def use_s2d(cin_g, kh, stride):
     """Space-to-depth for stride-2 stems on <= 4 channels (7x7/2, 3x3/2)."""
     return tuple(stride) == (2, 2) and 4 * cin_g <= 16 and kh > 1
+
+
+def s2d_kmask(kh, kw, cin_g, kpad, dev):
+    """K-mask of a space-to-depth packed row: 1 where byte (tap (a,b), channel (2u+v)*cin+ci)
+    is a real kernel tap (2a+u < kh, 2b+v < kw), else 0 (include/qnn.h, qnn_conv_desc.kmask)."""
+    pkw = (kw + 1) // 2
+    m = np.zeros(kpad, dtype=np.int8)
+    for a in range((kh + 1) // 2):
+        for b in range(pkw):
+            for uv in range(4):
+                u, v = uv >> 1, uv & 1
+                if 2 * a + u < kh and 2 * b + v < kw:
+                    base = (a * pkw + b) * 16 + uv * cin_g
+                    m[base:base + cin_g] = 1
+    return torch.from_numpy(m).to(dev)
 
 
 class _QLayerMixin:
@@ -293,6 +308,7 @@ class _QLayerMixin:
             pk.ptaps = kh * kw
         pk.cout_pad = _round_up(cout, 64) if cout <= 64 else _round_up(cout, 128)
         pk.kpad = _round_up(pk.ptaps * pk.cin_pad, 128)
+        pk.kmask = s2d_kmask(kh, kw, cin_g, pk.kpad, dev) if s2d else None
         pk.wq = torch.empty((pk.cout_pad, pk.kpad), dtype=torch.int8, device=dev)
         pk.s_w = torch.empty(cout, dtype=torch.float32, device=dev)
         pk.b_w = torch.empty(cout, dtype=torch.float32, device=dev)
@@ -409,6 +425,7 @@ class _QLayerMixin:
             _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, ph, d.cp, -float(mn), s,
                       qmax, st)
         d.zero_off = nbytes
+        d.kmask = None if pk.kmask is None else pk.kmask.data_ptr()
         g = self._geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev)
         sxsw, sxbw, table = self._epilogue(pk, g, (H, W), s32, b_x, kh, kw)
         y = torch.empty((N, cout, Ho, Wo), dtype=torch.float32, device=dev)

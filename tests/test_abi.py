@@ -84,7 +84,8 @@ def test_struct_layout_matches_header():
     import re as _re
     from qnn import _lib
     src = open(HEADER).read()
-    for cname, py in (("qnn_conv_desc", _lib.ConvDesc), ("qnn_epilogue", _lib.Epilogue)):
+    for cname, py in (("qnn_conv_desc", _lib.ConvDesc), ("qnn_epilogue", _lib.Epilogue),
+                      ("qnn_bn_params", _lib.BnParams), ("qnn_code_out", _lib.CodeOut)):
         body = _re.search(r"typedef struct " + cname + r" \{(.*?)\} " + cname, src, _re.S).group(1)
         body = _re.sub(r"/\*.*?\*/", "", body, flags=_re.S)
         names = []

@@ -1,0 +1,94 @@
+"""Fused whole-network engine (qnn/engine.py) on the GPU.
+
+* The engine evaluates the same contraction and restates the same elementwise
+  chain (RangeBN eval -> residual -> ReLU -> requantize, code-domain max-pool,
+  fused depthwise) as the module path, so the feature map entering the
+  classifier head must be BITWISE equal to the module path's — whose every layer
+  is checked against the oracle in tests/test_gpu_parity.py.
+* Logits: the drift-calibrated end-to-end bar against the reference's golden
+  logits (tests/test_gpu_parity.py docstring), and close to the module path
+  (only the avg-pool summation order differs).
+* Graph replay is deterministic and batch-size independent per sample.
+"""
+import glob
+import os
+
+import pytest
+import torch
+
+from conftest import GOLDEN, load_fixture
+from fixtures_util import build_model, e2e_tolerance, oracle_fp64_drift
+from oracle import qnn_oracle as O
+from qnn.engine import Engine
+
+pytestmark = pytest.mark.gpu
+MODELS = sorted(os.path.basename(p)[6:-4] for p in glob.glob(os.path.join(GOLDEN, "model_*.npz")))
+
+
+def _module_path(model, x):
+    feats = {}
+    pool = model.avg_pool if hasattr(model, "avg_pool") else model.avgpool
+    h = pool.register_forward_hook(lambda m, i, o: feats.setdefault("x", i[0].detach().clone()))
+    with torch.no_grad():
+        logits = model(x)
+    h.remove()
+    return logits, feats["x"]
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_engine_matches_module_path_and_reference(gpu, name):
+    d = load_fixture("model_" + name)
+    model, x = build_model(d)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    ref = torch.from_numpy(d["logits"])
+    model = model.to(gpu)
+    xg = x.to(gpu)
+    mod_logits, mod_feat = _module_path(model, xg)
+    eng = Engine(model, batch=x.shape[0])
+    logits = eng(xg).clone()
+    # bitwise: every fused epilogue, the code-domain max-pool and the fused depthwise
+    assert torch.equal(eng.head_input, mod_feat.permute(0, 2, 3, 1)), "engine feature map != module path"
+    # close to the module path (avg-pool order only)
+    dm = (logits - mod_logits).abs().max().item()
+    assert dm <= 1e-2 * mod_logits.abs().max().item(), dm
+    # end-to-end vs the reference
+    drift, _ = oracle_fp64_drift(O, sd, x, d["config"]["factory"], d["config"]["kw"], ref)
+    err = (logits.cpu() - ref).abs().max().item()
+    assert err <= e2e_tolerance(ref, drift), (err, drift)
+    # graph replay is deterministic
+    again = eng(xg).clone()
+    assert torch.equal(again, logits)
+
+
+def test_engine_batch_independence(gpu):
+    """Per-sample results do not depend on the batch they run in (the DP sharding
+    contract): batch 4 == 2 x batch 2, bitwise."""
+    d = load_fixture("model_resnet18_cifar")
+    model, _ = build_model(d)
+    model = model.to(gpu)
+    from qnn import synthetic
+    x = synthetic.input_batch((4, 3, 32, 32), 77).to(gpu)
+    full = Engine(model, batch=4)(x).clone()
+    half = Engine(model, batch=2)
+    a = half(x[:2]).clone()
+    b = half(x[2:]).clone()
+    assert torch.equal(full, torch.cat([a, b]))
+
+
+def test_engine_launch_count_resnet18(gpu):
+    from qnn import synthetic
+    from qnn.resnet_quantized import resnet_quantized
+    m = resnet_quantized(depth=18, dataset="imagenet")
+    synthetic.init_params(m, 1)
+    for mod in m.modules():
+        if hasattr(mod, "running_min"):
+            mod.running_min.fill_(0.0)
+            mod.running_max.fill_(2.0)
+        if type(mod).__name__ == "RangeBN":
+            mod.running_var.fill_(0.5)
+    m = m.to(gpu).eval()
+    eng = Engine(m, batch=2, graph=False)
+    # s2d quantize + stem conv + maxpool + 20 block convs (incl. 3 downsample) - stem + avgpool + fc
+    assert eng.num_launches == 1 + 1 + 1 + 19 + 1 + 1
+    y = eng()
+    assert torch.isfinite(y).all()
