@@ -93,6 +93,7 @@ class Engine:
         hp, wp = act.H + 2 * pad, act.W + 2 * pad
         nbytes = self.N * hp * wp * cp
         buf = torch.zeros(nbytes + 128, dtype=torch.int8, device=self.dev)
+        self.keep.append(buf)  # the engine owns every buffer its graph touches
         mn, mx = conv.quantize_input._eval_range()
         co = _lib.CodeOut(ptr=buf.data_ptr(), cp=cp, pad=pad, hp=hp, wp=wp, neg_min=-float(mn),
                           scale=float_scale(mn, mx, conv.num_bits), qmax=_qmax(conv.num_bits))
@@ -103,6 +104,7 @@ class Engine:
     def _f32_for(self, act):
         if act.f32 is None:
             act.f32 = torch.empty((self.N, act.H, act.W, act.C), dtype=torch.float32, device=self.dev)
+            self.keep.append(act.f32)
         return act.f32
 
     def _bn(self, bn):
@@ -211,6 +213,7 @@ class Engine:
             hz = Ho - 1 + (kh + 1) // 2
             nbytes = N * hz * hz * 16
             zbuf = torch.zeros(nbytes + 128, dtype=torch.int8, device=self.dev)
+            self.keep.append(zbuf)
             src = ("s2d", zbuf, dict(hp=hz, wp=hz, cp=16, nbytes=nbytes, range=(mn, mx)))
             xin, s, q = _lib.ptr(self.input), float_scale(mn, mx, conv1.num_bits), _qmax(conv1.num_bits)
             args = (N, 3, H, W, ph, hz, hz, -float(mn), s, q)
@@ -234,6 +237,7 @@ class Engine:
             mp = model.maxpool
             pk_, ps_, pp_ = mp.kernel_size, mp.stride, mp.padding
             bncode = torch.empty((N, Ho, Wo, conv1.out_channels), dtype=torch.uint8, device=self.dev)
+            self.keep.append(bncode)
             self._conv(conv1, src, H, W, bn=bn1, relu=True, out_bncode=bncode)
             Hp_ = (Ho + 2 * pp_ - pk_) // ps_ + 1
             x_act = _Act(Hp_, Hp_, conv1.out_channels)
@@ -272,6 +276,7 @@ class Engine:
         if blk.downsample is not None:
             ds_conv, ds_bn = blk.downsample[0], blk.downsample[1]
             r = torch.empty((N, Ho, Wo, cout), dtype=torch.float32, device=self.dev)
+            self.keep.append(r)
             self._conv(ds_conv, self._codes_for(x, ds_conv), x.H, x.W, bn=ds_bn, relu=False, out_f32=r)
             residual = r
         else:
@@ -337,6 +342,7 @@ class Engine:
         hz = Ho - 1 + (kh + 1) // 2
         nbytes = N * hz * hz * 16
         zbuf = torch.zeros(nbytes + 128, dtype=torch.int8, device=self.dev)
+        self.keep.append(zbuf)
         xin, s, q = _lib.ptr(self.input), float_scale(mn, mx, stem.num_bits), _qmax(stem.num_bits)
         args = (N, 3, H, W, ph, hz, hz, -float(mn), s, q)
         zp = _lib.ptr(zbuf)

@@ -28,7 +28,10 @@ MODELS = sorted(os.path.basename(p)[6:-4] for p in glob.glob(os.path.join(GOLDEN
 def _module_path(model, x):
     feats = {}
     pool = model.avg_pool if hasattr(model, "avg_pool") else model.avgpool
-    h = pool.register_forward_hook(lambda m, i, o: feats.setdefault("x", i[0].detach().clone()))
+    def grab(m, i, o):  # a hook must return None (a returned value replaces the output)
+        feats["x"] = i[0].detach().clone()
+
+    h = pool.register_forward_hook(grab)
     with torch.no_grad():
         logits = model(x)
     h.remove()
