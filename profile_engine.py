@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Per-launch profile of the fused engine: every kernel of one ResNet forward,
+HIP-event timed on its launch stream, with the conv's GEMM shape, int8 TOP/s and
+algorithmic GB/s (codes in + weights + codes/fp32 out).
+
+    python profile_engine.py [--depth 18] [--batch 128] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "quantized.pytorch_amd"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from qnn import _lib, synthetic  # noqa: E402
+from qnn.engine import Engine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--depth", type=int, default=18)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    _lib.load()
+    model = bench.build(dev, a.depth)
+    eng = Engine(model, batch=a.batch, graph=False)
+    eng.input.copy_(synthetic.input_batch((a.batch, 3, 224, 224), 1234).to(dev))
+    descs = [k for k in eng.keep if isinstance(k, _lib.ConvDesc)]
+    timer = _lib.LaunchTimer(set(eng.launch_names))
+    with torch.no_grad():
+        eng()
+        _lib.set_timer(timer)
+        for _ in range(a.reps):
+            eng()
+        _lib.set_timer(None)
+    d = timer.durations_ms()
+    n = len(eng.ops)
+    rows = []
+    ci = 0
+    for i in range(n):
+        name = d[i][0]
+        ms = sum(d[r * n + i][1] for r in range(a.reps)) / a.reps
+        row = {"i": i, "kernel": name, "us": round(ms * 1e3, 2)}
+        if name == "qnn_qconv2d_fwd":
+            c = descs[ci]
+            ci += 1
+            M = c.n * c.ho * c.wo
+            K = c.kh * c.kw * c.cp
+            ops = 2 * M * c.cout * K
+            row.update(MxNxK=[M, c.cout, K], tops=round(ops / ms / 1e9, 1), frac=round(ops / ms / 1e9 / 5000, 4))
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    tot = sum(r["us"] for r in rows)
+    conv = sum(r["us"] for r in rows if r["kernel"] == "qnn_qconv2d_fwd")
+    print(json.dumps({"total_us": round(tot, 1), "conv_us": round(conv, 1), "launches": n}))
+
+
+if __name__ == "__main__":
+    main()
