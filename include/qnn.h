@@ -164,6 +164,9 @@ typedef struct qnn_epilogue {
   int8_t* out_code1;
   int code1_cp, code1_pad, code1_hp, code1_wp;
   float code1_neg_min, code1_scale, code1_qmax;
+  const int8_t* lut;  /* nullable [cout][256]: out_code0 = lut[c][RangeBN input code] — the
+                         whole RangeBN -> ReLU -> consumer-quantizer chain tabulated per
+                         channel (qnn_bn_code_lut); needs bn, out_code0 only, no residual */
 } qnn_epilogue;
 
 /* Eval forward of QConv2d / QLinear (quantize.py:314-349, :398-428; biprecision's
@@ -210,6 +213,13 @@ typedef struct qnn_code_out {
   int cp, pad, hp, wp;
   float neg_min, scale, qmax;
 } qnn_code_out;
+
+/* Per-channel code -> code table of the chain RangeBN eval -> [ReLU] -> consumer quantizer
+ * (quantize.py:461-499 then :89-95), evaluated with the same device arithmetic as the
+ * fused epilogue: lut[c][q] = code'(relu(f_c(q)); next range) for q in 0..255.
+ * It makes the chain exact AND division-free in the conv epilogue. */
+int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,
+                    qnn_stream_t stream);
 
 /* ResNet stem max-pool (nn.MaxPool2d(3, 2, 1), resnet_quantized.py:174) fused with the
  * ReLU and RangeBN before it (:140-143), on RangeBN's input codes q [n][h][w][c] (uint8,

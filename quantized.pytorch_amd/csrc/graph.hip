@@ -119,6 +119,16 @@ __global__ void dwconv_fused_kernel(const int8_t* __restrict__ x, int n, int h, 
   }
 }
 
+// ------------------------------------------------------------------ RangeBN -> code LUT
+__global__ void bn_code_lut_kernel(qnn_bn_params bn, int c, int relu, qnn_code_out nx, int8_t* lut) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c * 256) return;
+  const int ch = i >> 8, q = i & 255;
+  float v = bn_apply((float)q, bn, ch);
+  if (relu) v = fmaxf(v, 0.f);
+  lut[i] = (int8_t)((int)quant_code(v, nx.neg_min, nx.scale, nx.qmax) - 128);
+}
+
 // ------------------------------------------------------------------ avg-pool head
 __global__ void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c, float* out_f32,
                                      qnn_code_out c0) {
@@ -206,6 +216,16 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
                      (hipStream_t)stream, x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min,
                      x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0);
   QNN_LAUNCH_CHECK("qnn_dwconv_fused");
+  return QNN_OK;
+}
+
+int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,
+                    qnn_stream_t stream) {
+  QNN_REQUIRE(c > 0 && bn && bn->mean && bn->sq && bn->wq && bn->bq && bn->scale > 0.f, "bad RangeBN params");
+  QNN_REQUIRE(next && next->scale > 0.f && lut, "bad next range / null lut");
+  hipLaunchKernelGGL(bn_code_lut_kernel, dim3((unsigned)cdiv((int64_t)c * 256, 256)), dim3(256), 0,
+                     (hipStream_t)stream, *bn, c, relu, *next, lut);
+  QNN_LAUNCH_CHECK("qnn_bn_code_lut");
   return QNN_OK;
 }
 

@@ -22,6 +22,8 @@
 // Block: 256 threads = 4 waves, each wave a 64x64 tile (2x2 MFMA 32x32x32).
 // K stage = 128 bytes; two LDS stages filled by LDS-DMA, counted vmcnt, raw
 // s_barrier; rows XOR-swizzled so ds_read_b128 fragment reads are conflict-free.
+#include <stdlib.h>
+
 #include "qnn_internal.h"
 
 namespace qnn {
@@ -30,10 +32,10 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int BK = 128;         // bytes of K per LDS stage (4 MFMA k-steps of 32)
 constexpr int MAX_TAPS = 64;
-constexpr int MAX_CLASSES = 64;
+constexpr int MAX_CLASSES = 32;
 constexpr int MAX_MASK = 1024;
+constexpr int KPAD_ALIGN = 128;  // packed weight rows are multiples of 128 bytes (any BK divides)
 
 struct Params {
   qnn_conv_desc d;
@@ -44,7 +46,15 @@ struct Params {
   int nstage;   // kpad / BK
 };
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// Byte offset of 16-byte chunk `chunk` of LDS row `row` (rows of BK bytes): XOR swizzle so
+// that the 16-lane groups of a ds_read_b128 fragment read (16 rows, one chunk) hit 16
+// distinct 16-B bank slots: BK=128 (2 rows per 256-B bank row) xor (row>>1)&7,
+// BK=64 (4 rows per bank row) xor (row>>2)&3.
+template <int BK>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  if constexpr (BK == 128) return row * BK + ((chunk ^ ((row >> 1) & 7)) << 4);
+  else return row * BK + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -52,24 +62,29 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-__device__ __forceinline__ void store_code4(int8_t* p, float4 v, float nm, float s, float qmax) {
-  int b0 = (int)quant_code(v.x, nm, s, qmax) - 128;
-  int b1 = (int)quant_code(v.y, nm, s, qmax) - 128;
-  int b2 = (int)quant_code(v.z, nm, s, qmax) - 128;
-  int b3 = (int)quant_code(v.w, nm, s, qmax) - 128;
+__device__ __forceinline__ void store_code4(int8_t* p, float4 v, float nm, float s, float inv, float qmax) {
+  int b0 = (int)quant_code_fast(v.x, nm, s, inv, qmax) - 128;
+  int b1 = (int)quant_code_fast(v.y, nm, s, inv, qmax) - 128;
+  int b2 = (int)quant_code_fast(v.z, nm, s, inv, qmax) - 128;
+  int b3 = (int)quant_code_fast(v.w, nm, s, inv, qmax) - 128;
   *reinterpret_cast<int*>(p) = (b0 & 255) | ((b1 & 255) << 8) | ((b2 & 255) << 16) | ((b3 & 255) << 24);
 }
 
-template <int BM, int BN, bool FUSED, bool MASKED>
+template <int BM, int BN, int BK, bool FUSED, bool MASKED>
 __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                     const Params p) {
   constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == 4, "4 waves of 64x64");
-  constexpr int NA = BM / 32;  // glds per wave per stage for A (1 KiB = 8 rows each)
-  constexpr int NB = BN / 32;
+  static_assert(BK == 64 || BK == 128, "BK");
+  constexpr int CPR = BK / 16;    // 16-B chunks per LDS row
+  constexpr int RPI = 1024 / BK;  // rows per 1 KiB LDS-DMA wave-instruction
+  constexpr int NA = BM / (4 * RPI);  // glds per wave per stage for A
+  constexpr int NB = BN / (4 * RPI);
   constexpr int STAGE = (BM + BN) * BK;
+  constexpr int MAIN = 2 * STAGE + 4 * MAX_TAPS + (MASKED ? MAX_MASK : 0);
+  constexpr int EPI = 4 * (7 + MAX_CLASSES) * BM + (FUSED ? 256 * BM : 0);  // params, border table, LUT
   // one LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) int8_t smem[2 * STAGE + 4 * MAX_TAPS + (MASKED ? MAX_MASK : 0)];
+  __shared__ __attribute__((aligned(16))) int8_t smem[MAIN > EPI ? MAIN : EPI];
   int* s_tap = reinterpret_cast<int*>(smem + 2 * STAGE);
   int8_t* s_mask = smem + 2 * STAGE + 4 * MAX_TAPS;
 
@@ -102,18 +117,18 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
   int bchunk[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int row = 8 * (wave + 4 * j) + (lane >> 3);
+    const int row = RPI * (wave + 4 * j) + lane / CPR;
     int m = m0 + row;
     if (m > p.M - 1) m = p.M - 1;
     const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
     boff[j] = (uint32_t)(((n * d.hp + ho * d.sh) * d.wp + wo * d.sw) * d.cp);
-    bchunk[j] = (lane & 7) ^ ((row >> 1) & 7);
+    bchunk[j] = (swz<BK>(row, lane % CPR) - row * BK) >> 4;  // the chunk that lands in this lane's slot
   }
   const int8_t* aptr[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int row = 8 * (wave + 4 * j) + (lane >> 3);
-    aptr[j] = w + (int64_t)(c0 + row) * d.kpad + 16 * ((lane & 7) ^ ((row >> 1) & 7));
+    const int row = RPI * (wave + 4 * j) + lane / CPR;
+    aptr[j] = w + (int64_t)(c0 + row) * d.kpad + (swz<BK>(row, lane % CPR) - row * BK);
   }
   const int cpt_mask = (1 << p.lgcpt) - 1;
   __syncthreads();  // s_tap
@@ -127,7 +142,7 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
                                        (lds_ptr_t)(sa + (wave + 4 * j) * 1024), 16, 0, 0);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int kc = st * 8 + bchunk[j];
+      const int kc = st * CPR + bchunk[j];
       const int tap = kc >> p.lgcpt;
       uint32_t off = tap < p.taps ? boff[j] + (uint32_t)s_tap[tap] + (uint32_t)((kc & cpt_mask) << 4)
                                   : (uint32_t)d.zero_off;
@@ -145,9 +160,10 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
 
   const int frow = lane & 31, fh = lane >> 5;
   issue(0, 0);
-  for (int st = 0; st < p.nstage; ++st) {
+  const int nstage = p.d.kpad / BK;
+  for (int st = 0; st < nstage; ++st) {
     const int buf = st & 1;
-    if (st + 1 < p.nstage) {
+    if (st + 1 < nstage) {
       issue(st + 1, buf ^ 1);
       wait_vmcnt<NA + NB>();
     } else {
@@ -157,14 +173,14 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
     const int8_t* sa = smem + buf * STAGE;
     const int8_t* sb = sa + BM * BK;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < BK / 32; ++ks) {
       const int chunk = 2 * ks + fh;
       v4i fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz(wm * 64 + i * 32 + frow, chunk));
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz<BK>(wm * 64 + i * 32 + frow, chunk));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        fb[j] = *reinterpret_cast<const v4i*>(sb + swz(wn * 64 + j * 32 + frow, chunk));
+        fb[j] = *reinterpret_cast<const v4i*>(sb + swz<BK>(wn * 64 + j * 32 + frow, chunk));
         v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
         if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(s_mask + st * BK + 16 * chunk);
         int s = __builtin_amdgcn_sdot4(fb[j].x, ones.x, sumq[j], false);
@@ -202,7 +218,16 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
     const int cls = i / BM, c = c0 + (i - cls * BM);
     s_f[nparam + i] = c < d.cout ? e.table[cls * d.cout + c] : 0.f;
   }
+  int8_t* s_lut = smem + 4 * (7 + MAX_CLASSES) * BM;  // [BM][256] next-layer codes (FUSED && e.lut)
+  if (FUSED && e.lut) {
+    for (int i = tid; i < BM * 16; i += 256) {
+      const int c = c0 + (i >> 4);
+      if (c < d.cout)
+        *reinterpret_cast<v4i*>(s_lut + 16 * i) = *reinterpret_cast<const v4i*>(e.lut + (int64_t)c * 256 + 16 * (i & 15));
+    }
+  }
   __syncthreads();
+  const float bn_inv = 1.0f / e.bn_scale, c0_inv = 1.0f / e.code0_scale, c1_inv = 1.0f / e.code1_scale;
 #pragma unroll
   for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
 
@@ -234,12 +259,23 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
           continue;
         }
         if (c >= d.cout) continue;  // cout % 4 == 0 in fused mode
+        if (e.lut) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated per channel (exact)
+          int r = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
+            r |= ((int)(uint8_t)s_lut[(cl + u) * 256 + q]) << (8 * u);
+          }
+          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
+          *reinterpret_cast<int*>(e.out_code0 + a) = r;
+          continue;
+        }
         if (e.bn_mean) {
           int qb[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int l = cl + u;
-            const float q = quant_code(v[u], e.bn_neg_min, e.bn_scale, e.bn_qmax);  // RangeBN.quantize_input
+            const float q = quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN.quantize_input
             qb[u] = (int)q;
             float o = dequant(q, e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
             o = o * s_f[4 * BM + l];                                         // * q(scale)
@@ -261,24 +297,42 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
         if (e.out_f32) *reinterpret_cast<float4*>(e.out_f32 + (int64_t)m * d.cout + c) = o4;
         if (e.out_code0) {
           const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
-          store_code4(e.out_code0 + a, o4, e.code0_neg_min, e.code0_scale, e.code0_qmax);
+          store_code4(e.out_code0 + a, o4, e.code0_neg_min, e.code0_scale, c0_inv, e.code0_qmax);
         }
         if (e.out_code1) {
           const int64_t a = (((int64_t)n * e.code1_hp + ho + e.code1_pad) * e.code1_wp + wo + e.code1_pad) * e.code1_cp + c;
-          store_code4(e.out_code1 + a, o4, e.code1_neg_min, e.code1_scale, e.code1_qmax);
+          store_code4(e.out_code1 + a, o4, e.code1_neg_min, e.code1_scale, c1_inv, e.code1_qmax);
         }
       }
     }
   }
 }
 
-template <int BM, int BN, bool FUSED>
+template <int BM, int BN, int BK, bool FUSED>
 static void launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
   if (p.d.kmask)
-    hipLaunchKernelGGL((qconv_kernel<BM, BN, FUSED, true>), dim3(nblk), dim3(256), 0, s, x, w, p);
+    hipLaunchKernelGGL((qconv_kernel<BM, BN, BK, FUSED, true>), dim3(nblk), dim3(256), 0, s, x, w, p);
   else
-    hipLaunchKernelGGL((qconv_kernel<BM, BN, FUSED, false>), dim3(nblk), dim3(256), 0, s, x, w, p);
+    hipLaunchKernelGGL((qconv_kernel<BM, BN, BK, FUSED, false>), dim3(nblk), dim3(256), 0, s, x, w, p);
+}
+
+// K-stage depth: 64-byte stages halve the LDS of a block (more blocks per CU to hide
+// DMA latency and overlap one block's epilogue with another's MFMAs).  QNN_CONV_BK
+// overrides (64 / 128) for A/B measurements.
+static int pick_bk(const Params& p) {
+  static int forced = [] {
+    const char* v = getenv("QNN_CONV_BK");
+    return v ? atoi(v) : 0;
+  }();
+  if (forced == 64 || forced == 128) return forced;
+  return 64;
+}
+
+template <int BM, int BN, bool FUSED>
+static void launch_bk(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (pick_bk(p) == 128) launch<BM, BN, 128, FUSED>(x, w, p, s);
+  else launch<BM, BN, 64, FUSED>(x, w, p, s);
 }
 
 }  // namespace qnn
@@ -296,7 +350,7 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   QNN_REQUIRE(d.kh * d.kw <= MAX_TAPS, "at most 64 taps");
   QNN_REQUIRE(d.ho > 0 && d.wo > 0 && (d.ho - 1) * d.sh + d.kh <= d.hp && (d.wo - 1) * d.sw + d.kw <= d.wp,
               "ho/wo exceed the padded input");
-  QNN_REQUIRE(d.kpad % BK == 0 && d.kpad >= d.kh * d.kw * d.cp, "kpad must be a multiple of 128 covering K");
+  QNN_REQUIRE(d.kpad % KPAD_ALIGN == 0 && d.kpad >= d.kh * d.kw * d.cp, "kpad must be a multiple of 128 covering K");
   QNN_REQUIRE((int64_t)d.n * d.hp * d.wp * d.cp < (1LL << 31) && d.zero_off >= 0 && d.zero_off % 16 == 0,
               "input too large or bad zero_off");
   QNN_REQUIRE(!d.kmask || (d.kpad <= MAX_MASK && (((uintptr_t)d.kmask) & 15) == 0), "kmask: kpad <= 1024, 16-B aligned");
@@ -313,6 +367,9 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
     QNN_REQUIRE(!e.out_code0 || (e.code0_cp % 4 == 0 && e.code0_scale > 0.f), "bad code0");
     QNN_REQUIRE(!e.out_code1 || (e.code1_cp % 4 == 0 && e.code1_scale > 0.f), "bad code1");
     QNN_REQUIRE(e.out_f32 || e.out_code0 || e.out_code1 || e.out_bncode, "fused mode without an output");
+    QNN_REQUIRE(!e.lut || (e.bn_mean && e.out_code0 && !e.residual && !e.out_f32 && !e.out_code1 && !e.out_bncode &&
+                           (((uintptr_t)e.lut) & 15) == 0),
+                "lut needs RangeBN, exactly one code output, no residual/fp32/bncode, 16-B aligned");
   }
   Params p;
   p.d = d;
@@ -322,16 +379,16 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   p.M = (int)M;
   p.taps = d.kh * d.kw;
   p.lgcpt = __builtin_ctz(d.cp / 16);
-  p.nstage = d.kpad / BK;
+  p.nstage = 0;
   hipStream_t s = (hipStream_t)stream;
   const bool narrow = d.cout <= 64;
   QNN_REQUIRE(d.cout_pad >= (narrow ? 64 : 128) * (int)cdiv(d.cout, narrow ? 64 : 128), "cout_pad too small");
   if (e.mode == 0) {
-    if (narrow) launch<64, 256, false>(x, wq, p, s);
-    else launch<128, 128, false>(x, wq, p, s);
+    if (narrow) launch_bk<64, 256, false>(x, wq, p, s);
+    else launch_bk<128, 128, false>(x, wq, p, s);
   } else {
-    if (narrow) launch<64, 256, true>(x, wq, p, s);
-    else launch<128, 128, true>(x, wq, p, s);
+    if (narrow) launch_bk<64, 256, true>(x, wq, p, s);
+    else launch_bk<128, 128, true>(x, wq, p, s);
   }
   QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
   return QNN_OK;

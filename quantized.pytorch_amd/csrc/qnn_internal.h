@@ -38,6 +38,19 @@ __device__ __forceinline__ float quant_code(float x, float neg_min, float scale,
   return rintf(u);                 // round_()  half-to-even  :95
 }
 
+// quant_code without a per-element IEEE division, bit-identical to quant_code:
+// u = t * inv_scale (inv_scale = fl(1/scale)) is within 1.5 ulp of fl(t/scale), i.e.
+// |u - u*| < 2^-14 for |u| <= 256.  rint(clamp(.)) can differ from the exact one only
+// if a half-integer lies between u and u*, which forces |u - rint(u)| > 0.5 - 2^-14;
+// every such lane (and exact ties) takes the exact division (about 0.2 % of lanes).
+__device__ __forceinline__ float quant_code_fast(float x, float neg_min, float scale, float inv_scale, float qmax) {
+  const float t = x + neg_min;
+  const float uc = fminf(fmaxf(t * inv_scale, 0.0f), qmax);
+  const float r = rintf(uc);
+  if (fabsf(uc - r) > 0.4990234375f) return quant_code(x, neg_min, scale, qmax);
+  return r;
+}
+
 __device__ __forceinline__ float dequant(float q, float scale, float min) {
   float v = q * scale;             // add_(-qmin).mul_(scale) :100
   return v + min;                  // add_(min_value)         :100

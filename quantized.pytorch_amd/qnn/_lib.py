@@ -37,7 +37,8 @@ class Epilogue(ctypes.Structure):
                 ("out_code0", c_ptr), ("code0_cp", c_int), ("code0_pad", c_int), ("code0_hp", c_int),
                 ("code0_wp", c_int), ("code0_neg_min", c_float), ("code0_scale", c_float), ("code0_qmax", c_float),
                 ("out_code1", c_ptr), ("code1_cp", c_int), ("code1_pad", c_int), ("code1_hp", c_int),
-                ("code1_wp", c_int), ("code1_neg_min", c_float), ("code1_scale", c_float), ("code1_qmax", c_float)]
+                ("code1_wp", c_int), ("code1_neg_min", c_float), ("code1_scale", c_float), ("code1_qmax", c_float),
+                ("lut", c_ptr)]
 
 class BnParams(ctypes.Structure):
     """qnn_bn_params (include/qnn.h)."""
@@ -73,6 +74,7 @@ SIGNATURES = {
     "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
+    "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],
     "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr, c_int, c_ptr],
 }

@@ -169,6 +169,13 @@ class Engine:
                     setattr(e, f"code{k}_{f}", getattr(co, f))
                 setattr(e, f"out_code{k}", co.ptr)
             assert len(outs) <= 2
+            if bn is not None and residual is None and out_f32 is None and out_bncode is None and len(outs) == 1:
+                # conv -> RangeBN -> ReLU -> consumer quantizer: one exact per-channel code table
+                lut = torch.empty((cout, 256), dtype=torch.int8, device=self.dev)
+                _lib.call("qnn_bn_code_lut", ctypes.byref(b), cout, 1 if relu else 0, ctypes.byref(outs[0]),
+                          _lib.ptr(lut), _lib.stream_of(lut))
+                e.lut = lut.data_ptr()
+                self.keep.append(lut)
         xbuf = src[1] if s2d else src[0]
         self.keep += [pk, sxsw, sxbw, table, g, d, e, xbuf]
         xp, wp_, dp, ep = _lib.ptr(xbuf), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e)
