@@ -221,16 +221,21 @@ typedef struct qnn_code_out {
 int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,
                     qnn_stream_t stream);
 
-/* ResNet stem max-pool (nn.MaxPool2d(3, 2, 1), resnet_quantized.py:174) fused with the
- * ReLU and RangeBN before it (:140-143), on RangeBN's input codes q [n][h][w][c] (uint8,
- * written by the stem conv's epilogue as out_bncode).  With
- *   f_c(q) = fl(fl(fl(dequant(q) - mean) * sq) * wq) + bq,  g = relu o f_c,
- * g is monotone per channel (direction sign(sq*wq)), so max over the window of
- * g(q_i) = g(max q_i) (or g(min q_i)) exactly; padding positions are skipped (-inf).
- * Outputs: out_f32 NHWC [n][ho][wo][c] (nullable) and codes for up to two consumers. */
-int qnn_maxpool_bncode(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
-                       const qnn_bn_params* bn, int relu, float* out_f32, const qnn_code_out* code0,
-                       const qnn_code_out* code1, qnn_stream_t stream);
+/* Per-channel value table and monotonicity of g = [relu o] RangeBN_eval on its input code:
+ * vlut[c][q] = g_c(q) (fp32, quantize.py:484-499 op order), dir[c] = 1 when g_c is
+ * non-increasing (sign(sq*wq) < 0), else 0. */
+int qnn_bn_value_lut(const qnn_bn_params* bn, int c, int relu, float* vlut, uint8_t* dir, qnn_stream_t stream);
+
+/* ResNet stem max-pool (nn.MaxPool2d(k, stride, pad), resnet_quantized.py:174) fused with
+ * the ReLU and RangeBN before it (:140-143), on RangeBN's input codes q [n][h][w][c]
+ * (uint8, the stem conv's out_bncode).  g_c is monotone, so max over the window of
+ * g_c(q_i) = g_c(max q_i) (min where dir[c]); padding positions are skipped (-inf).
+ * Outputs: out_f32 = vlut[c][q*] NHWC [n][ho][wo][c] (nullable; needs vlut) and codes
+ * lut{0,1}[c][q*] (qnn_bn_code_lut) into consumer buffers code{0,1} (nullable). */
+int qnn_maxpool_lut(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
+                    const uint8_t* dir, const float* vlut, float* out_f32, const int8_t* lut0,
+                    const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                    qnn_stream_t stream);
 
 /* Depthwise QConv2d (groups == c, mobilenet_quantized.py:38-40) fused with its RangeBN and
  * ReLU (:41-42) on padded NHWC8 codes x [n][hp][wp][cp] whose image interior is

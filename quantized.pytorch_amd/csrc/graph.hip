@@ -32,15 +32,26 @@ __device__ __forceinline__ void decode_pix(int64_t i, int cg, int wo, int ho, in
 }
 
 // ------------------------------------------------------------------ max-pool on RangeBN codes
-__global__ void maxpool_bncode_kernel(const uint8_t* __restrict__ q, int n, int h, int w, int c, int k, int stride,
-                                      int pad, int ho, int wo, qnn_bn_params bn, int relu, float* out_f32,
-                                      qnn_code_out c0, qnn_code_out c1) {
+__device__ __forceinline__ void put_lut4(const qnn_code_out& o, const int8_t* __restrict__ lut, int n, int h, int w,
+                                         int c, const int q[4]) {
+  int8_t* p = o.ptr + (((int64_t)n * o.hp + h + o.pad) * o.wp + w + o.pad) * o.cp + c;
+  int r = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r |= ((int)(uint8_t)lut[(c + u) * 256 + q[u]]) << (8 * u);
+  *reinterpret_cast<int*>(p) = r;
+}
+
+__global__ void maxpool_lut_kernel(const uint8_t* __restrict__ q, int n, int h, int w, int c, int k, int stride,
+                                   int pad, int ho, int wo, const uint8_t* __restrict__ dir,
+                                   const float* __restrict__ vlut, float* out_f32, const int8_t* __restrict__ lut0,
+                                   qnn_code_out c0, const int8_t* __restrict__ lut1, qnn_code_out c1) {
   const int cg = c >> 2;
   const int64_t total = (int64_t)n * ho * wo * cg;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     int g, ox, oy, img;
     decode_pix(i, cg, wo, ho, g, ox, oy, img);
     const int cbase = 4 * g;
+    const uint32_t dmask = *reinterpret_cast<const uint32_t*>(dir + cbase);  // 1 byte per channel
     int hi4[4] = {-1, -1, -1, -1}, lo4[4] = {256, 256, 256, 256};
     for (int r = 0; r < k; ++r) {
       const int iy = oy * stride - pad + r;
@@ -57,20 +68,26 @@ __global__ void maxpool_bncode_kernel(const uint8_t* __restrict__ q, int n, int 
         }
       }
     }
-    float val[4];
+    int qs[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ch = cbase + u;
-      const bool dec = (bn.sq[ch] * bn.wq[ch]) < 0.f;  // g = relu o f_c non-increasing
-      const float o = bn_apply((float)(dec ? lo4[u] : hi4[u]), bn, ch);
-      val[u] = relu ? fmaxf(o, 0.f) : o;
+    for (int u = 0; u < 4; ++u) qs[u] = ((dmask >> (8 * u)) & 255) ? lo4[u] : hi4[u];
+    if (out_f32) {
+      const float4 o = make_float4(vlut[(cbase + 0) * 256 + qs[0]], vlut[(cbase + 1) * 256 + qs[1]],
+                                   vlut[(cbase + 2) * 256 + qs[2]], vlut[(cbase + 3) * 256 + qs[3]]);
+      *reinterpret_cast<float4*>(out_f32 + (((int64_t)img * ho + oy) * wo + ox) * c + cbase) = o;
     }
-    if (out_f32)
-      *reinterpret_cast<float4*>(out_f32 + (((int64_t)img * ho + oy) * wo + ox) * c + cbase) =
-          make_float4(val[0], val[1], val[2], val[3]);
-    if (c0.ptr) put_code4(c0, img, oy, ox, cbase, val);
-    if (c1.ptr) put_code4(c1, img, oy, ox, cbase, val);
+    if (c0.ptr) put_lut4(c0, lut0, img, oy, ox, cbase, qs);
+    if (c1.ptr) put_lut4(c1, lut1, img, oy, ox, cbase, qs);
   }
+}
+
+__global__ void bn_value_lut_kernel(qnn_bn_params bn, int c, int relu, float* vlut, uint8_t* dir) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c * 256) return;
+  const int ch = i >> 8, qv = i & 255;
+  float v = bn_apply((float)qv, bn, ch);
+  vlut[i] = relu ? fmaxf(v, 0.f) : v;
+  if (qv == 0) dir[ch] = (bn.sq[ch] * bn.wq[ch]) < 0.f ? 1 : 0;
 }
 
 // ------------------------------------------------------------------ depthwise, fused
@@ -176,20 +193,33 @@ using namespace qnn;
 
 extern "C" {
 
-int qnn_maxpool_bncode(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
-                       const qnn_bn_params* bn, int relu, float* out_f32, const qnn_code_out* code0,
-                       const qnn_code_out* code1, qnn_stream_t stream) {
+int qnn_bn_value_lut(const qnn_bn_params* bn, int c, int relu, float* vlut, uint8_t* dir, qnn_stream_t stream) {
+  QNN_REQUIRE(c > 0 && bn && bn->mean && bn->sq && bn->wq && bn->bq && bn->scale > 0.f, "bad RangeBN params");
+  QNN_REQUIRE(vlut && dir, "null output");
+  hipLaunchKernelGGL(bn_value_lut_kernel, dim3((unsigned)cdiv((int64_t)c * 256, 256)), dim3(256), 0,
+                     (hipStream_t)stream, *bn, c, relu, vlut, dir);
+  QNN_LAUNCH_CHECK("qnn_bn_value_lut");
+  return QNN_OK;
+}
+
+int qnn_maxpool_lut(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
+                    const uint8_t* dir, const float* vlut, float* out_f32, const int8_t* lut0,
+                    const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                    qnn_stream_t stream) {
   QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
   QNN_REQUIRE(ho == (h + 2 * pad - k) / stride + 1 && wo == (w + 2 * pad - k) / stride + 1, "ho/wo inconsistent");
-  QNN_REQUIRE(bn && bn->mean && bn->sq && bn->wq && bn->bq && bn->scale > 0.f, "bad RangeBN params");
+  QNN_REQUIRE(dir && (((uintptr_t)dir) & 3) == 0, "dir must be non-null and 4-byte aligned");
+  QNN_REQUIRE(!out_f32 || vlut, "out_f32 needs vlut");
+  QNN_REQUIRE(!(code0 && code0->ptr) || lut0, "code0 needs lut0");
+  QNN_REQUIRE(!(code1 && code1->ptr) || lut1, "code1 needs lut1");
   if (int rc = check_code(code0, c, "bad code0")) return rc;
   if (int rc = check_code(code1, c, "bad code1")) return rc;
   if (n == 0) return QNN_OK;
   QNN_REQUIRE(q, "null input");
   const qnn_code_out c0 = code0 ? *code0 : none_code(), c1 = code1 ? *code1 : none_code();
-  hipLaunchKernelGGL(maxpool_bncode_kernel, dim3(grid_for((int64_t)n * ho * wo * (c / 4))), dim3(256), 0,
-                     (hipStream_t)stream, q, n, h, w, c, k, stride, pad, ho, wo, *bn, relu, out_f32, c0, c1);
-  QNN_LAUNCH_CHECK("qnn_maxpool_bncode");
+  hipLaunchKernelGGL(maxpool_lut_kernel, dim3(grid_for((int64_t)n * ho * wo * (c / 4))), dim3(256), 0,
+                     (hipStream_t)stream, q, n, h, w, c, k, stride, pad, ho, wo, dir, vlut, out_f32, lut0, c0, lut1, c1);
+  QNN_LAUNCH_CHECK("qnn_maxpool_lut");
   return QNN_OK;
 }
 

@@ -231,25 +231,45 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
 #pragma unroll
   for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
 
+  // per-pixel (lane) state for the two 32-pixel column tiles of this wave
+  int pm[2], pn[2], phw[2], pho[2], pwo[2], ptab[2];
+  float psq[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int m = m0 + wn * 64 + j * 32 + frow;
-    if (m >= p.M) continue;
-    const int n = m / HoWo, hw = m - n * HoWo, ho = hw / d.wo, wo = hw - ho * d.wo;
-    const float* trow = s_f + nparam + (e.hcls[ho] * e.nwc + e.wcls[wo]) * BM;
-    const float sq = (float)sumq[j];
+    pm[j] = m;
+    const int mm = m < p.M ? m : p.M - 1;
+    pn[j] = mm / HoWo;
+    phw[j] = mm - pn[j] * HoWo;
+    pho[j] = phw[j] / d.wo;
+    pwo[j] = phw[j] - pho[j] * d.wo;
+    ptab[j] = nparam + (e.hcls[pho[j]] * e.nwc + e.wcls[pwo[j]]) * BM;
+    psq[j] = (float)sumq[j];
+  }
+  // channel groups outer (params loaded once), pixel tiles inner
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 2; ++i) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g
-        const int c = c0 + cl;
+    for (int g = 0; g < 4; ++g) {
+      const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
+      const int c = c0 + cl;
+      if (FUSED && c >= d.cout) continue;  // cout % 4 == 0 in fused mode
+      float a_sxsw[4], a_sxbw[4], a_bias[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a_sxsw[u] = s_f[cl + u];
+        a_sxbw[u] = s_f[BM + cl + u];
+        a_bias[u] = s_f[2 * BM + cl + u];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (pm[j] >= p.M) continue;
+        const int m = pm[j], n = pn[j], hw = phw[j], ho = pho[j], wo = pwo[j];
         float v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int l = cl + u;
-          float y = fmaf(s_f[l], (float)acc[i][j][4 * g + u], fmaf(s_f[BM + l], sq, trow[l]));
-          v[u] = y + s_f[2 * BM + l];
+          const float y = fmaf(a_sxsw[u], (float)acc[i][j][4 * g + u], fmaf(a_sxbw[u], psq[j], s_f[ptab[j] + cl + u]));
+          v[u] = y + a_bias[u];
         }
         if (!FUSED) {
           float* yp = e.out_f32 + ((int64_t)n * d.cout + c) * HoWo + hw;
@@ -258,7 +278,6 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
             if (c + u < d.cout) yp[(int64_t)u * HoWo] = v[u];
           continue;
         }
-        if (c >= d.cout) continue;  // cout % 4 == 0 in fused mode
         if (e.lut) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated per channel (exact)
           int r = 0;
 #pragma unroll
@@ -273,18 +292,21 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
         if (e.bn_mean) {
           int qb[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int l = cl + u;
-            const float q = quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN.quantize_input
-            qb[u] = (int)q;
-            float o = dequant(q, e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
-            o = o * s_f[4 * BM + l];                                         // * q(scale)
-            o = o * s_f[5 * BM + l];                                         // * q(weight)
-            v[u] = o + s_f[6 * BM + l];                                      // + q(bias)
-          }
-          if (e.out_bncode)
+          for (int u = 0; u < 4; ++u)
+            qb[u] = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN.quantize_input
+          if (e.out_bncode) {
             *reinterpret_cast<int*>(e.out_bncode + (int64_t)m * d.cout + c) =
                 qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24);
+            if (!e.out_f32 && !e.out_code0) continue;  // stem before the code-domain max-pool
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int l = cl + u;
+            float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
+            o = o * s_f[4 * BM + l];                                                   // * q(scale)
+            o = o * s_f[5 * BM + l];                                                   // * q(weight)
+            v[u] = o + s_f[6 * BM + l];                                                // + q(bias)
+          }
         }
         float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
         if (e.residual) {
@@ -326,7 +348,7 @@ static int pick_bk(const Params& p) {
     return v ? atoi(v) : 0;
   }();
   if (forced == 64 || forced == 128) return forced;
-  return 64;
+  return p.d.cout <= 64 ? 64 : 128;  // measured: BK=64 wins on 64-channel layers, 128 on wider
 }
 
 template <int BM, int BN, bool FUSED>

@@ -69,8 +69,9 @@ SIGNATURES = {
     "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
-    "qnn_maxpool_bncode": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,
-                           _PC, _PC, c_ptr],
+    "qnn_bn_value_lut": [_PB, c_int, c_int, c_ptr, c_ptr, c_ptr],
+    "qnn_maxpool_lut": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr,
+                        c_ptr, _PC, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_ptr, _PC, c_ptr],

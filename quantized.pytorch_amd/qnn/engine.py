@@ -251,15 +251,27 @@ class Engine:
             cons, need_f32 = self._block_consumers(blocks[0])
             outs, f32 = self._outputs(x_act, cons, need_f32)
             b = self._bn(bn1)
+            C = conv1.out_channels
+            st = _lib.stream_of(self.input)
+            dirs = torch.empty(C, dtype=torch.uint8, device=self.dev)
+            vlut = torch.empty((C, 256), dtype=torch.float32, device=self.dev)
+            _lib.call("qnn_bn_value_lut", ctypes.byref(b), C, 1, _lib.ptr(vlut), _lib.ptr(dirs), st)
+            luts = []
+            for co in outs:
+                lut = torch.empty((C, 256), dtype=torch.int8, device=self.dev)
+                _lib.call("qnn_bn_code_lut", ctypes.byref(b), C, 1, ctypes.byref(co), _lib.ptr(lut), st)
+                luts.append(lut)
+            self.keep += [bncode, dirs, vlut] + luts + list(outs)
             c0 = outs[0] if len(outs) > 0 else None
             c1 = outs[1] if len(outs) > 1 else None
-            self.keep += [bncode, c0, c1]
-            a = (N, Ho, Wo, conv1.out_channels, pk_, ps_, pp_, Hp_, Hp_)
-            fp, qp = _lib.ptr(f32), _lib.ptr(bncode)
+            a = (N, Ho, Wo, C, pk_, ps_, pp_, Hp_, Hp_)
+            fp, qp, dp, vp = _lib.ptr(f32), _lib.ptr(bncode), _lib.ptr(dirs), _lib.ptr(vlut)
+            l0 = _lib.ptr(luts[0]) if len(luts) > 0 else None
+            l1 = _lib.ptr(luts[1]) if len(luts) > 1 else None
             r0 = None if c0 is None else ctypes.byref(c0)
             r1 = None if c1 is None else ctypes.byref(c1)
-            self._add("qnn_maxpool_bncode", lambda st: _lib.call(
-                "qnn_maxpool_bncode", qp, *a, ctypes.byref(b), 1, fp, r0, r1, st))
+            self._add("qnn_maxpool_lut", lambda st: _lib.call(
+                "qnn_maxpool_lut", qp, *a, dp, vp, fp, l0, r0, l1, r1, st))
         else:
             x_act = _Act(Ho, Wo, conv1.out_channels)
             cons, need_f32 = self._block_consumers(blocks[0])
