@@ -70,6 +70,145 @@ __device__ __forceinline__ void store_code4(int8_t* p, float4 v, float nm, float
   *reinterpret_cast<int*>(p) = (b0 & 255) | ((b1 & 255) << 8) | ((b2 & 255) << 16) | ((b3 & 255) << 24);
 }
 
+// Epilogue shared by the implicit-GEMM and halo kernels.  sumq[j]: full receptive-field
+// sum of q'_x for this lane's pixel of column tile j.  smem: >= epilogue LDS bytes.
+template <int BM, bool FUSED>
+__device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], const int (&sumq)[2], int8_t* smem,
+                                         int m0, int c0, int wm, int wn, int lane) {
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, frow = lane & 31, fh = lane >> 5;
+  const int HoWo = d.ho * d.wo;
+  const qnn_epilogue& e = p.e;
+  float* s_f = reinterpret_cast<float*>(smem);  // main-loop LDS is free now
+  // [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq  [7BM..) table[cls][BM]
+  const int nparam = 7 * BM;
+  for (int i = tid; i < BM; i += 256) {
+    const int c = c0 + i;
+    const bool ok = c < d.cout;
+    s_f[i] = ok ? e.sxsw[c] : 0.f;
+    s_f[BM + i] = ok ? e.sxbw[c] : 0.f;
+    s_f[2 * BM + i] = (ok && e.bias) ? e.bias[c] : 0.f;
+    if (FUSED && e.bn_mean) {
+      s_f[3 * BM + i] = ok ? e.bn_mean[c] : 0.f;
+      s_f[4 * BM + i] = ok ? e.bn_sq[c] : 0.f;
+      s_f[5 * BM + i] = ok ? e.bn_wq[c] : 0.f;
+      s_f[6 * BM + i] = ok ? e.bn_bq[c] : 0.f;
+    }
+  }
+  for (int i = tid; i < e.nclass * BM; i += 256) {
+    const int cls = i / BM, c = c0 + (i - cls * BM);
+    s_f[nparam + i] = c < d.cout ? e.table[cls * d.cout + c] : 0.f;
+  }
+  int8_t* s_lut = smem + 4 * (7 + MAX_CLASSES) * BM;  // [BM][256] next-layer codes (FUSED && e.lut)
+  if (FUSED && e.lut) {
+    for (int i = tid; i < BM * 16; i += 256) {
+      const int c = c0 + (i >> 4);
+      if (c < d.cout)
+        *reinterpret_cast<v4i*>(s_lut + 16 * i) = *reinterpret_cast<const v4i*>(e.lut + (int64_t)c * 256 + 16 * (i & 15));
+    }
+  }
+  __syncthreads();
+  const float bn_inv = 1.0f / e.bn_scale, c0_inv = 1.0f / e.code0_scale, c1_inv = 1.0f / e.code1_scale;
+
+  // per-pixel (lane) state for the two 32-pixel column tiles of this wave
+  int pm[2], pn[2], phw[2], pho[2], pwo[2], ptab[2];
+  float psq[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + wn * 64 + j * 32 + frow;
+    pm[j] = m;
+    const int mm = m < p.M ? m : p.M - 1;
+    pn[j] = mm / HoWo;
+    phw[j] = mm - pn[j] * HoWo;
+    pho[j] = phw[j] / d.wo;
+    pwo[j] = phw[j] - pho[j] * d.wo;
+    ptab[j] = nparam + (e.hcls[pho[j]] * e.nwc + e.wcls[pwo[j]]) * BM;
+    psq[j] = (float)sumq[j];
+  }
+  // channel groups outer (params loaded once), pixel tiles inner
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
+      const int c = c0 + cl;
+      if (FUSED && c >= d.cout) continue;  // cout % 4 == 0 in fused mode
+      float a_sxsw[4], a_sxbw[4], a_bias[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a_sxsw[u] = s_f[cl + u];
+        a_sxbw[u] = s_f[BM + cl + u];
+        a_bias[u] = s_f[2 * BM + cl + u];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (pm[j] >= p.M) continue;
+        const int m = pm[j], n = pn[j], hw = phw[j], ho = pho[j], wo = pwo[j];
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float y = fmaf(a_sxsw[u], (float)acc[i][j][4 * g + u], fmaf(a_sxbw[u], psq[j], s_f[ptab[j] + cl + u]));
+          v[u] = y + a_bias[u];
+        }
+        if (!FUSED) {
+          float* yp = e.out_f32 + ((int64_t)n * d.cout + c) * HoWo + hw;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (c + u < d.cout) yp[(int64_t)u * HoWo] = v[u];
+          continue;
+        }
+        if (e.lut) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated per channel (exact)
+          int r = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
+            r |= ((int)(uint8_t)s_lut[(cl + u) * 256 + q]) << (8 * u);
+          }
+          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
+          *reinterpret_cast<int*>(e.out_code0 + a) = r;
+          continue;
+        }
+        if (e.bn_mean) {
+          int qb[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            qb[u] = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN.quantize_input
+          if (e.out_bncode) {
+            *reinterpret_cast<int*>(e.out_bncode + (int64_t)m * d.cout + c) =
+                qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24);
+            if (!e.out_f32 && !e.out_code0) continue;  // stem before the code-domain max-pool
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int l = cl + u;
+            float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
+            o = o * s_f[4 * BM + l];                                                   // * q(scale)
+            o = o * s_f[5 * BM + l];                                                   // * q(weight)
+            v[u] = o + s_f[6 * BM + l];                                                // + q(bias)
+          }
+        }
+        float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
+        if (e.residual) {
+          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + (int64_t)m * d.cout + c);
+          o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
+        }
+        if (e.relu) {
+          o4.x = fmaxf(o4.x, 0.f); o4.y = fmaxf(o4.y, 0.f); o4.z = fmaxf(o4.z, 0.f); o4.w = fmaxf(o4.w, 0.f);
+        }
+        if (e.out_f32) *reinterpret_cast<float4*>(e.out_f32 + (int64_t)m * d.cout + c) = o4;
+        if (e.out_code0) {
+          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
+          store_code4(e.out_code0 + a, o4, e.code0_neg_min, e.code0_scale, c0_inv, e.code0_qmax);
+        }
+        if (e.out_code1) {
+          const int64_t a = (((int64_t)n * e.code1_hp + ho + e.code1_pad) * e.code1_wp + wo + e.code1_pad) * e.code1_cp + c;
+          store_code4(e.out_code1 + a, o4, e.code1_neg_min, e.code1_scale, c1_inv, e.code1_qmax);
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int BK, bool FUSED, bool MASKED>
 __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                     const Params p) {
@@ -197,136 +336,236 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
   }
 
   // ================================================================ epilogue
-  const qnn_epilogue& e = p.e;
-  float* s_f = reinterpret_cast<float*>(smem);  // main-loop LDS is free now
-  // [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq  [7BM..) table[cls][BM]
-  const int nparam = 7 * BM;
-  for (int i = tid; i < BM; i += 256) {
-    const int c = c0 + i;
-    const bool ok = c < d.cout;
-    s_f[i] = ok ? e.sxsw[c] : 0.f;
-    s_f[BM + i] = ok ? e.sxbw[c] : 0.f;
-    s_f[2 * BM + i] = (ok && e.bias) ? e.bias[c] : 0.f;
-    if (FUSED && e.bn_mean) {
-      s_f[3 * BM + i] = ok ? e.bn_mean[c] : 0.f;
-      s_f[4 * BM + i] = ok ? e.bn_sq[c] : 0.f;
-      s_f[5 * BM + i] = ok ? e.bn_wq[c] : 0.f;
-      s_f[6 * BM + i] = ok ? e.bn_bq[c] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
+  __syncthreads();  // main-loop LDS is reused by the epilogue
+  epilogue<BM, FUSED>(p, acc, sumq, smem, m0, c0, wm, wn, lane);
+}
+
+// ============================================================================ halo kernel
+// For kh x kw convs with Cp >= 32 (the ResNet 3x3s).  The implicit-GEMM kernel above
+// re-gathers every activation byte once per tap (9x for 3x3) through L1, which caps
+// it at the per-CU load bandwidth.  Here a block loads, per channel chunk of CK bytes,
+// the BAND of padded input rows covering its pixel tile's receptive field into LDS
+// ONCE (rows [n0*hp + ho0*sh, n1*hp + ho1*sh + kh - 1] of the flattened padded
+// buffer, every column, CK channels), then serves all kh*kw taps' B fragments from
+// it; only the per-tap weight slice [BM][CK] streams (LDS-DMA, double-buffered).
+// sum_valid(q'_x) comes from per-band-pixel channel sums S[q] (one v_dot4 pass per
+// band pixel instead of one per fragment), summed over the taps of each pixel.
+constexpr int MAX_BAND = 40960;
+
+template <int CPR>
+__device__ __forceinline__ int swz_c(int idx, int chunk) {
+  // chunk slot of 16-B chunk `chunk` in LDS row `idx` (rows of 16*CPR bytes): conflict-free
+  // ds_read_b128 over 16 consecutive rows
+  return chunk ^ ((idx / (16 / CPR)) & (CPR - 1));
+}
+
+template <int BM, int BN, int CK, bool FUSED>
+__global__ __launch_bounds__(256) void qconv_halo_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+                                                         const Params p) {
+  constexpr int WM = BM / 64, WN = BN / 64;
+  static_assert(WM * WN == 4, "4 waves of 64x64");
+  constexpr int CPR = CK / 16;
+  constexpr int A_BYTES = BM * CK;
+  constexpr int NPA = A_BYTES / 1024;  // 1-KiB LDS-DMA pieces per weight slice
+  static_assert(NPA % 4 == 0, "every wave issues the same number of weight pieces");
+  constexpr int BAND_PIX = MAX_BAND / CK;
+  constexpr int OFF_S = MAX_BAND + 1024;            // band + slack for a partial last piece
+  constexpr int OFF_A = OFF_S + 4 * BAND_PIX;
+  constexpr int MAIN = OFF_A + 2 * A_BYTES;
+  constexpr int EPI = 4 * (7 + MAX_CLASSES) * BM + (FUSED ? 256 * BM : 0);
+  __shared__ __attribute__((aligned(16))) int8_t smem[MAIN > EPI ? MAIN : EPI];
+  int8_t* s_band = smem;
+  int* s_sum = reinterpret_cast<int*>(smem + OFF_S);
+  int8_t* s_a = smem + OFF_A;
+
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int frow = lane & 31, fh = lane >> 5;
+
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nblk = ((p.M + BN - 1) / BN) * nby;
+  int t;
+  {
+    const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int m0 = (t / nby) * BN;
+  const int c0 = (t % nby) * BM;
+  const int HoWo = d.ho * d.wo;
+
+  // band rows of this pixel tile (flattened padded rows n*hp + row)
+  int rlo, rhi;
+  {
+    const int mA = m0, mB = min(m0 + BN, p.M) - 1;
+    const int nA = mA / HoWo, hoA = (mA - nA * HoWo) / d.wo;
+    const int nB = mB / HoWo, hoB = (mB - nB * HoWo) / d.wo;
+    rlo = nA * d.hp + hoA * d.sh;
+    rhi = nB * d.hp + hoB * d.sh + d.kh - 1;
+  }
+  const int band_pix = (rhi - rlo + 1) * d.wp;
+  const int band_pieces = (band_pix * CK + 1023) >> 10;
+  const int8_t* xband = x + (int64_t)rlo * d.wp * d.cp;
+
+  // per-lane band pixel of tap (0,0) for the two 32-pixel column tiles
+  int P[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int m = m0 + wn * 64 + j * 32 + frow;
+    if (m > p.M - 1) m = p.M - 1;
+    const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
+    P[j] = (n * d.hp + ho * d.sh - rlo) * d.wp + wo * d.sw;
+  }
+  // per-lane A fragment row offsets (fixed)
+  int arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) arow[i] = wm * 64 + i * 32 + frow;
+
+  const int taps = p.taps;
+  const int nch = d.cp / CK;
+  const int nsteps = nch * taps;
+
+  auto issue_a = [&](int step, int buf) {
+    const int ch = step / taps, tp = step - ch * taps;
+    const int8_t* src = w + (int64_t)c0 * d.kpad + tp * d.cp + ch * CK;
+#pragma unroll
+    for (int k = 0; k < NPA / 4; ++k) {
+      const int pc = wave + 4 * k;
+      const int L = pc * 64 + lane, row = L / CPR, slot = L % CPR;
+      __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)row * d.kpad + 16 * swz_c<CPR>(row, slot)),
+                                       (lds_ptr_t)(s_a + buf * A_BYTES + pc * 1024), 16, 0, 0);
     }
-  }
-  for (int i = tid; i < e.nclass * BM; i += 256) {
-    const int cls = i / BM, c = c0 + (i - cls * BM);
-    s_f[nparam + i] = c < d.cout ? e.table[cls * d.cout + c] : 0.f;
-  }
-  int8_t* s_lut = smem + 4 * (7 + MAX_CLASSES) * BM;  // [BM][256] next-layer codes (FUSED && e.lut)
-  if (FUSED && e.lut) {
-    for (int i = tid; i < BM * 16; i += 256) {
-      const int c = c0 + (i >> 4);
-      if (c < d.cout)
-        *reinterpret_cast<v4i*>(s_lut + 16 * i) = *reinterpret_cast<const v4i*>(e.lut + (int64_t)c * 256 + 16 * (i & 15));
+  };
+  auto issue_band = [&](int ch) {
+    const int8_t* src = xband + ch * CK;
+    for (int pc = wave; pc < band_pieces; pc += 4) {
+      const int L = pc * 64 + lane, q = L / CPR, slot = L % CPR;
+      uint32_t off = q < band_pix ? (uint32_t)(q * d.cp + 16 * swz_c<CPR>(q, slot))
+                                  : (uint32_t)(d.zero_off - (int64_t)rlo * d.wp * d.cp - ch * CK);
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((const void*)(src + off), (lds_ptr_t)(s_band + pc * 1024), 16, 0, 0);
+    }
+  };
+
+  v16i acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (v16i){0};
+  int sumq[2] = {0, 0};
+
+  issue_a(0, 0);
+  for (int ch = 0; ch < nch; ++ch) {
+    issue_band(ch);
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    // per-band-pixel channel sums of the codes (exact)
+    for (int q = tid; q < band_pix; q += 256) {
+      int ssum = 0;
+#pragma unroll
+      for (int c = 0; c < CPR; ++c) {
+        const v4i v = *reinterpret_cast<const v4i*>(s_band + q * CK + 16 * c);
+        ssum = __builtin_amdgcn_sdot4(v.x, 0x01010101, ssum, false);
+        ssum = __builtin_amdgcn_sdot4(v.y, 0x01010101, ssum, false);
+        ssum = __builtin_amdgcn_sdot4(v.z, 0x01010101, ssum, false);
+        ssum = __builtin_amdgcn_sdot4(v.w, 0x01010101, ssum, false);
+      }
+      s_sum[q] = ssum;
+    }
+    __syncthreads();
+    for (int tp = 0; tp < taps; ++tp) {
+      const int step = ch * taps + tp;
+      const int buf = step & 1;
+      if (step + 1 < nsteps) {
+        issue_a(step + 1, buf ^ 1);
+        wait_vmcnt<NPA / 4>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      const int r = tp / d.kw, sx = tp - r * d.kw;
+      const int toff = r * d.wp + sx;
+      const int8_t* sa = s_a + buf * A_BYTES;
+      int bidx[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bidx[j] = P[j] + toff;
+        sumq[j] += s_sum[bidx[j]];
+      }
+#pragma unroll
+      for (int ks = 0; ks < CK / 32; ++ks) {
+        const int chunk = 2 * ks + fh;
+        v4i fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          fa[i] = *reinterpret_cast<const v4i*>(sa + arow[i] * CK + 16 * swz_c<CPR>(arow[i], chunk));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          fb[j] = *reinterpret_cast<const v4i*>(s_band + bidx[j] * CK + 16 * swz_c<CPR>(bidx[j], chunk));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_barrier();
     }
   }
   __syncthreads();
-  const float bn_inv = 1.0f / e.bn_scale, c0_inv = 1.0f / e.code0_scale, c1_inv = 1.0f / e.code1_scale;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
+  epilogue<BM, FUSED>(p, acc, sumq, smem, m0, c0, wm, wn, lane);
+}
 
-  // per-pixel (lane) state for the two 32-pixel column tiles of this wave
-  int pm[2], pn[2], phw[2], pho[2], pwo[2], ptab[2];
-  float psq[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int m = m0 + wn * 64 + j * 32 + frow;
-    pm[j] = m;
-    const int mm = m < p.M ? m : p.M - 1;
-    pn[j] = mm / HoWo;
-    phw[j] = mm - pn[j] * HoWo;
-    pho[j] = phw[j] / d.wo;
-    pwo[j] = phw[j] - pho[j] * d.wo;
-    ptab[j] = nparam + (e.hcls[pho[j]] * e.nwc + e.wcls[pwo[j]]) * BM;
-    psq[j] = (float)sumq[j];
+// Largest band (bytes per channel byte) over the pixel tiles of one launch.
+static int64_t max_band_rows(const Params& p, int BN) {
+  const qnn_conv_desc& d = p.d;
+  const int HoWo = d.ho * d.wo;
+  int64_t worst = 0;
+  for (int m0 = 0; m0 < p.M; m0 += BN) {
+    const int mB = (m0 + BN < p.M ? m0 + BN : p.M) - 1;
+    const int nA = m0 / HoWo, hoA = (m0 - nA * HoWo) / d.wo;
+    const int nB = mB / HoWo, hoB = (mB - nB * HoWo) / d.wo;
+    const int64_t rows = (int64_t)(nB * d.hp + hoB * d.sh + d.kh - 1) - (nA * d.hp + hoA * d.sh) + 1;
+    if (rows > worst) worst = rows;
   }
-  // channel groups outer (params loaded once), pixel tiles inner
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
-      const int c = c0 + cl;
-      if (FUSED && c >= d.cout) continue;  // cout % 4 == 0 in fused mode
-      float a_sxsw[4], a_sxbw[4], a_bias[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a_sxsw[u] = s_f[cl + u];
-        a_sxbw[u] = s_f[BM + cl + u];
-        a_bias[u] = s_f[2 * BM + cl + u];
+  return worst;
+}
+
+template <int BM, int BN, int CK, bool FUSED>
+static void launch_halo(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
+  hipLaunchKernelGGL((qconv_halo_kernel<BM, BN, CK, FUSED>), dim3(nblk), dim3(256), 0, s, x, w, p);
+}
+
+// Picks the halo kernel's channel chunk (0 = not applicable).  QNN_HALO=0 disables it.
+static int pick_halo_ck(const Params& p, int BM, int BN) {
+  static int enabled = [] {
+    const char* v = getenv("QNN_HALO");
+    return v ? atoi(v) : 1;
+  }();
+  const qnn_conv_desc& d = p.d;
+  if (!enabled || d.kmask || d.kh * d.kw < 2 || d.cp < 32) return 0;
+  const int64_t rows = max_band_rows(p, BN);
+  for (int ck : {128, 64, 32}) {
+    if (d.cp % ck) continue;
+    if ((BM * ck / 1024) % 4) continue;
+    if (rows * d.wp * ck <= MAX_BAND) return ck;
+  }
+  return 0;
+}
+
+template <int BM, int BN, bool FUSED>
+static bool try_halo(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  switch (pick_halo_ck(p, BM, BN)) {
+    case 128: launch_halo<BM, BN, 128, FUSED>(x, w, p, s); return true;
+    case 64: launch_halo<BM, BN, 64, FUSED>(x, w, p, s); return true;
+    case 32:
+      if constexpr (BM == 128) {
+        launch_halo<BM, BN, 32, FUSED>(x, w, p, s);
+        return true;
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (pm[j] >= p.M) continue;
-        const int m = pm[j], n = pn[j], hw = phw[j], ho = pho[j], wo = pwo[j];
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float y = fmaf(a_sxsw[u], (float)acc[i][j][4 * g + u], fmaf(a_sxbw[u], psq[j], s_f[ptab[j] + cl + u]));
-          v[u] = y + a_bias[u];
-        }
-        if (!FUSED) {
-          float* yp = e.out_f32 + ((int64_t)n * d.cout + c) * HoWo + hw;
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (c + u < d.cout) yp[(int64_t)u * HoWo] = v[u];
-          continue;
-        }
-        if (e.lut) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated per channel (exact)
-          int r = 0;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
-            r |= ((int)(uint8_t)s_lut[(cl + u) * 256 + q]) << (8 * u);
-          }
-          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
-          *reinterpret_cast<int*>(e.out_code0 + a) = r;
-          continue;
-        }
-        if (e.bn_mean) {
-          int qb[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            qb[u] = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN.quantize_input
-          if (e.out_bncode) {
-            *reinterpret_cast<int*>(e.out_bncode + (int64_t)m * d.cout + c) =
-                qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24);
-            if (!e.out_f32 && !e.out_code0) continue;  // stem before the code-domain max-pool
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int l = cl + u;
-            float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
-            o = o * s_f[4 * BM + l];                                                   // * q(scale)
-            o = o * s_f[5 * BM + l];                                                   // * q(weight)
-            v[u] = o + s_f[6 * BM + l];                                                // + q(bias)
-          }
-        }
-        float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
-        if (e.residual) {
-          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + (int64_t)m * d.cout + c);
-          o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
-        }
-        if (e.relu) {
-          o4.x = fmaxf(o4.x, 0.f); o4.y = fmaxf(o4.y, 0.f); o4.z = fmaxf(o4.z, 0.f); o4.w = fmaxf(o4.w, 0.f);
-        }
-        if (e.out_f32) *reinterpret_cast<float4*>(e.out_f32 + (int64_t)m * d.cout + c) = o4;
-        if (e.out_code0) {
-          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
-          store_code4(e.out_code0 + a, o4, e.code0_neg_min, e.code0_scale, c0_inv, e.code0_qmax);
-        }
-        if (e.out_code1) {
-          const int64_t a = (((int64_t)n * e.code1_hp + ho + e.code1_pad) * e.code1_wp + wo + e.code1_pad) * e.code1_cp + c;
-          store_code4(e.out_code1 + a, o4, e.code1_neg_min, e.code1_scale, c1_inv, e.code1_qmax);
-        }
-      }
-    }
+      return false;
+    default: return false;
   }
 }
 
@@ -353,6 +592,7 @@ static int pick_bk(const Params& p) {
 
 template <int BM, int BN, bool FUSED>
 static void launch_bk(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (try_halo<BM, BN, FUSED>(x, w, p, s)) return;
   if (pick_bk(p) == 128) launch<BM, BN, 128, FUSED>(x, w, p, s);
   else launch<BM, BN, 64, FUSED>(x, w, p, s);
 }
