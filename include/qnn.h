@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 2
+#define QNN_ABI_VERSION 3
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -135,11 +135,18 @@ typedef struct qnn_conv_desc {
  * mode 1 (fused model graph, resnet_quantized.py:52-68/:93-113, mobilenet_quantized.py:38-48):
  *   v = bn_mean ? RangeBN_eval(y) : y     (quantize.py:461-499, exact fp32 op order;
  *                                          out_bncode receives RangeBN's input code)
- *   v = residual ? fl(v + residual) : v   (NHWC fp32 [m][cout])
+ *   v = residual ? fl(v + residual) : v   (fp32 [m][cout], NHWC or C-tile, see f32_tiled)
  *   v = relu ? max(v, 0) : v
- *   out_f32 = v (NHWC fp32 [m][cout]);  out_code{0,1} = codes of v for a consumer conv with
- *   QuantMeasure range (neg_min, scale, qmax), written into that consumer's padded NHWC8
- *   buffer [n][hp][wp][cp] at (ho + pad, wo + pad).  cout % 4 == 0. */
+ *   out_f32 = v (fp32 [m][cout], NHWC or C-tile);  out_code{0,1} = codes of v for a consumer
+ *   conv with QuantMeasure range (neg_min, scale, qmax), written into that consumer's padded
+ *   NHWC8 buffer [n][hp][wp][cp] at (ho + pad, wo + pad); channels [cout, cp) of every
+ *   16-byte group the block covers are written as code' 0.  cout % 16 == 0, cp % 16 == 0.
+ *
+ * C-tile layout (f32_tiled != 0): the fp32 image of the MFMA 32x32 accumulators, so the
+ * epilogue reads/writes it with one coalesced 1-KiB access per wave-instruction:
+ *   index(m, c) = (((m/32)*CT + c/32)*4 + (c%32)/8)*256 + (m%32 + 32*((c/4)%2))*4 + c%4
+ * with CT = ceil(cout/32); a map holds ceil(M/32)*32 * CT*32 floats.  Producer and
+ * consumer of a residual agree on it (qnn_maxpool_bn, qnn_avgpool_quant take it too). */
 typedef struct qnn_epilogue {
   int mode;
   const float* sxsw;
@@ -167,6 +174,7 @@ typedef struct qnn_epilogue {
   const int8_t* lut;  /* nullable [cout][256]: out_code0 = lut[c][RangeBN input code] — the
                          whole RangeBN -> ReLU -> consumer-quantizer chain tabulated per
                          channel (qnn_bn_code_lut); needs bn, out_code0 only, no residual */
+  int f32_tiled;      /* mode 1: residual and out_f32 in the C-tile layout (else NHWC)     */
 } qnn_epilogue;
 
 /* Eval forward of QConv2d / QLinear (quantize.py:314-349, :398-428; biprecision's
@@ -221,21 +229,17 @@ typedef struct qnn_code_out {
 int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,
                     qnn_stream_t stream);
 
-/* Per-channel value table and monotonicity of g = [relu o] RangeBN_eval on its input code:
- * vlut[c][q] = g_c(q) (fp32, quantize.py:484-499 op order), dir[c] = 1 when g_c is
- * non-increasing (sign(sq*wq) < 0), else 0. */
-int qnn_bn_value_lut(const qnn_bn_params* bn, int c, int relu, float* vlut, uint8_t* dir, qnn_stream_t stream);
-
 /* ResNet stem max-pool (nn.MaxPool2d(k, stride, pad), resnet_quantized.py:174) fused with
  * the ReLU and RangeBN before it (:140-143), on RangeBN's input codes q [n][h][w][c]
- * (uint8, the stem conv's out_bncode).  g_c is monotone, so max over the window of
- * g_c(q_i) = g_c(max q_i) (min where dir[c]); padding positions are skipped (-inf).
- * Outputs: out_f32 = vlut[c][q*] NHWC [n][ho][wo][c] (nullable; needs vlut) and codes
- * lut{0,1}[c][q*] (qnn_bn_code_lut) into consumer buffers code{0,1} (nullable). */
-int qnn_maxpool_lut(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
-                    const uint8_t* dir, const float* vlut, float* out_f32, const int8_t* lut0,
-                    const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
-                    qnn_stream_t stream);
+ * (uint8, the stem conv's out_bncode).  g_c = [relu o] RangeBN_eval is monotone in the
+ * code (non-increasing where sq*wq < 0), so max over the window of g_c(q_i) = g_c(max q_i)
+ * (min where decreasing); padding positions are skipped (-inf).  Outputs: out_f32 =
+ * g_c(q*) (fp32 [m][c], NHWC or C-tile by f32_tiled; nullable) and codes lut{0,1}[c][q*]
+ * (qnn_bn_code_lut) into consumer buffers code{0,1} (nullable).  c % 16 == 0. */
+int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
+                   const qnn_bn_params* bn, int relu, float* out_f32, int f32_tiled, const int8_t* lut0,
+                   const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                   qnn_stream_t stream);
 
 /* Depthwise QConv2d (groups == c, mobilenet_quantized.py:38-40) fused with its RangeBN and
  * ReLU (:41-42) on padded NHWC8 codes x [n][hp][wp][cp] whose image interior is
@@ -250,10 +254,11 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
                      const qnn_code_out* code0, qnn_stream_t stream);
 
 /* nn.AvgPool2d(k) over the whole k x k map (resnet_quantized.py:153, mobilenet_quantized.py:157)
- * on NHWC fp32 x [n][hw][c]: mean = (sum in row-major tap order) / hw; writes out_f32 [n][c]
+ * on fp32 x [n*hw][c] (NHWC, or the C-tile layout when x_tiled): mean = (sum in row-major
+ * tap order) / hw; writes out_f32 [n][c]
  * (nullable) and the codes of the classifier's QuantMeasure into code0 (hp = wp = 1). */
-int qnn_avgpool_quant(const float* x, int n, int hw, int c, float* out_f32, const qnn_code_out* code0,
-                      qnn_stream_t stream);
+int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* out_f32,
+                      const qnn_code_out* code0, qnn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -32,62 +32,111 @@ __device__ __forceinline__ void decode_pix(int64_t i, int cg, int wo, int ho, in
 }
 
 // ------------------------------------------------------------------ max-pool on RangeBN codes
-__device__ __forceinline__ void put_lut4(const qnn_code_out& o, const int8_t* __restrict__ lut, int n, int h, int w,
-                                         int c, const int q[4]) {
-  int8_t* p = o.ptr + (((int64_t)n * o.hp + h + o.pad) * o.wp + w + o.pad) * o.cp + c;
-  int r = 0;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) r |= ((int)(uint8_t)lut[(c + u) * 256 + q[u]]) << (8 * u);
-  *reinterpret_cast<int*>(p) = r;
+// One thread per (output pixel, 16 channels); consecutive lanes take consecutive
+// pixels so the C-tile fp32 stores are 512 contiguous bytes per 32 lanes.  The pool
+// direction per channel (max where g_c increases, min where it decreases) is folded
+// into the codes with an XOR (min q == 255 - max(255 - q)), so the window reduction is
+// a plain bytewise max (two packed-u16 maxes per dword).  RangeBN params and the
+// consumer code tables live in LDS.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t max_u8x4(uint32_t a, uint32_t b) {
+  u16x2 alo = __builtin_bit_cast(u16x2, a & 0x00ff00ffu), ahi = __builtin_bit_cast(u16x2, (a >> 8) & 0x00ff00ffu);
+  u16x2 blo = __builtin_bit_cast(u16x2, b & 0x00ff00ffu), bhi = __builtin_bit_cast(u16x2, (b >> 8) & 0x00ff00ffu);
+  u16x2 lo = __builtin_elementwise_max(alo, blo), hi = __builtin_elementwise_max(ahi, bhi);
+  return __builtin_bit_cast(uint32_t, lo) | (__builtin_bit_cast(uint32_t, hi) << 8);
 }
 
-__global__ void maxpool_lut_kernel(const uint8_t* __restrict__ q, int n, int h, int w, int c, int k, int stride,
-                                   int pad, int ho, int wo, const uint8_t* __restrict__ dir,
-                                   const float* __restrict__ vlut, float* out_f32, const int8_t* __restrict__ lut0,
-                                   qnn_code_out c0, const int8_t* __restrict__ lut1, qnn_code_out c1) {
-  const int cg = c >> 2;
-  const int64_t total = (int64_t)n * ho * wo * cg;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int g, ox, oy, img;
-    decode_pix(i, cg, wo, ho, g, ox, oy, img);
-    const int cbase = 4 * g;
-    const uint32_t dmask = *reinterpret_cast<const uint32_t*>(dir + cbase);  // 1 byte per channel
-    int hi4[4] = {-1, -1, -1, -1}, lo4[4] = {256, 256, 256, 256};
+__global__ __launch_bounds__(256) void maxpool_bn_kernel(const uint8_t* __restrict__ q, int n, int h, int w, int c,
+                                                         int k, int stride, int pad, int ho, int wo,
+                                                         qnn_bn_params bn, int relu, float* out_f32, int tiled,
+                                                         const int8_t* __restrict__ lut0, qnn_code_out c0,
+                                                         const int8_t* __restrict__ lut1, qnn_code_out c1) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  float* s_mean = reinterpret_cast<float*>(smem);
+  float* s_sq = s_mean + c;
+  float* s_wq = s_sq + c;
+  float* s_bq = s_wq + c;
+  uint8_t* s_dir = reinterpret_cast<uint8_t*>(s_bq + c);  // 0xff where g_c is non-increasing
+  int8_t* s_lut0 = reinterpret_cast<int8_t*>(s_dir + c);
+  int8_t* s_lut1 = s_lut0 + (lut0 ? c * 256 : 0);
+  for (int i = threadIdx.x; i < c; i += blockDim.x) {
+    s_mean[i] = bn.mean[i];
+    s_sq[i] = bn.sq[i];
+    s_wq[i] = bn.wq[i];
+    s_bq[i] = bn.bq[i];
+    s_dir[i] = (bn.sq[i] * bn.wq[i]) < 0.f ? 0xff : 0;
+  }
+  for (int i = threadIdx.x; i < c * 16; i += blockDim.x) {
+    if (lut0) reinterpret_cast<int4*>(s_lut0)[i] = reinterpret_cast<const int4*>(lut0)[i];
+    if (lut1) reinterpret_cast<int4*>(s_lut1)[i] = reinterpret_cast<const int4*>(lut1)[i];
+  }
+  __syncthreads();
+  const int kc = c >> 4, ct = (c + 31) >> 5;
+  const int64_t M = (int64_t)n * ho * wo;
+  const int64_t total = ((M + 31) >> 5) * kc * 32;
+  for (int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * blockDim.x) {
+    const int lo = (int)(gi & 31);
+    const int64_t rest = gi >> 5;
+    const int kg = (int)(rest % kc);
+    const int64_t m = (rest / kc) * 32 + lo;
+    if (m >= M) continue;
+    const int cb = 16 * kg;
+    const int ox = (int)(m % wo);
+    const int64_t t = m / wo;
+    const int oy = (int)(t % ho), img = (int)(t / ho);
+    const uint4 dm = *reinterpret_cast<const uint4*>(s_dir + cb);
+    uint4 best = make_uint4(0, 0, 0, 0);
     for (int r = 0; r < k; ++r) {
       const int iy = oy * stride - pad + r;
       if (iy < 0 || iy >= h) continue;  // MaxPool2d pads with -inf
-      for (int s = 0; s < k; ++s) {
-        const int ix = ox * stride - pad + s;
+      for (int s2 = 0; s2 < k; ++s2) {
+        const int ix = ox * stride - pad + s2;
         if (ix < 0 || ix >= w) continue;
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(q + (((int64_t)img * h + iy) * w + ix) * c + cbase);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int b = (v >> (8 * u)) & 255;
-          hi4[u] = max(hi4[u], b);
-          lo4[u] = min(lo4[u], b);
-        }
+        const uint4 v = *reinterpret_cast<const uint4*>(q + (((int64_t)img * h + iy) * w + ix) * c + cb);
+        best.x = max_u8x4(best.x, v.x ^ dm.x);
+        best.y = max_u8x4(best.y, v.y ^ dm.y);
+        best.z = max_u8x4(best.z, v.z ^ dm.z);
+        best.w = max_u8x4(best.w, v.w ^ dm.w);
       }
     }
-    int qs[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) qs[u] = ((dmask >> (8 * u)) & 255) ? lo4[u] : hi4[u];
+    const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
     if (out_f32) {
-      const float4 o = make_float4(vlut[(cbase + 0) * 256 + qs[0]], vlut[(cbase + 1) * 256 + qs[1]],
-                                   vlut[(cbase + 2) * 256 + qs[2]], vlut[(cbase + 3) * 256 + qs[3]]);
-      *reinterpret_cast<float4*>(out_f32 + (((int64_t)img * ho + oy) * wo + ox) * c + cbase) = o;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ch = cb + 4 * s4 + u;
+          float o = dequant((float)((qd[s4] >> (8 * u)) & 255), bn.scale, bn.min) - s_mean[ch];  // quantize.py:488
+          o = o * s_sq[ch];                                                                     // :488-489
+          o = o * s_wq[ch];                                                                     // :495
+          o = o + s_bq[ch];                                                                     // :499
+          v[u] = relu ? fmaxf(o, 0.f) : o;
+        }
+        const int64_t fi = tiled ? ctile_index(m, cb + 4 * s4, ct) : m * c + cb + 4 * s4;
+        *reinterpret_cast<float4*>(out_f32 + fi) = make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
-    if (c0.ptr) put_lut4(c0, lut0, img, oy, ox, cbase, qs);
-    if (c1.ptr) put_lut4(c1, lut1, img, oy, ox, cbase, qs);
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const qnn_code_out& co = o ? c1 : c0;
+      const int8_t* sl = o ? s_lut1 : s_lut0;
+      if (!co.ptr) continue;
+      int r[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        r[s4] = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ch = cb + 4 * s4 + u;
+          r[s4] |= ((int)(uint8_t)sl[ch * 256 + ((qd[s4] >> (8 * u)) & 255)]) << (8 * u);
+        }
+      }
+      *reinterpret_cast<int4*>(co.ptr + (((int64_t)img * co.hp + oy + co.pad) * co.wp + ox + co.pad) * co.cp + cb) =
+          make_int4(r[0], r[1], r[2], r[3]);
+    }
   }
-}
-
-__global__ void bn_value_lut_kernel(qnn_bn_params bn, int c, int relu, float* vlut, uint8_t* dir) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c * 256) return;
-  const int ch = i >> 8, qv = i & 255;
-  float v = bn_apply((float)qv, bn, ch);
-  vlut[i] = relu ? fmaxf(v, 0.f) : v;
-  if (qv == 0) dir[ch] = (bn.sq[ch] * bn.wq[ch]) < 0.f ? 1 : 0;
 }
 
 // ------------------------------------------------------------------ depthwise, fused
@@ -147,17 +196,18 @@ __global__ void bn_code_lut_kernel(qnn_bn_params bn, int c, int relu, qnn_code_o
 }
 
 // ------------------------------------------------------------------ avg-pool head
-__global__ void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c, float* out_f32,
+__global__ void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c, int tiled, float* out_f32,
                                      qnn_code_out c0) {
   const int cg = c >> 2;
   const int64_t total = (int64_t)n * cg;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int g = (int)(i % cg);
     const int img = (int)(i / cg);
-    const float* p = x + (int64_t)img * hw * c + 4 * g;
+    const int ct = (c + 31) >> 5;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int t = 0; t < hw; ++t) {
-      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)t * c);
+      const int64_t m = (int64_t)img * hw + t;
+      const float4 v = *reinterpret_cast<const float4*>(x + (tiled ? ctile_index(m, 4 * g, ct) : m * c + 4 * g));
       s.x = s.x + v.x; s.y = s.y + v.y; s.z = s.z + v.z; s.w = s.w + v.w;
     }
     const float d = (float)hw;
@@ -193,33 +243,38 @@ using namespace qnn;
 
 extern "C" {
 
-int qnn_bn_value_lut(const qnn_bn_params* bn, int c, int relu, float* vlut, uint8_t* dir, qnn_stream_t stream) {
-  QNN_REQUIRE(c > 0 && bn && bn->mean && bn->sq && bn->wq && bn->bq && bn->scale > 0.f, "bad RangeBN params");
-  QNN_REQUIRE(vlut && dir, "null output");
-  hipLaunchKernelGGL(bn_value_lut_kernel, dim3((unsigned)cdiv((int64_t)c * 256, 256)), dim3(256), 0,
-                     (hipStream_t)stream, *bn, c, relu, vlut, dir);
-  QNN_LAUNCH_CHECK("qnn_bn_value_lut");
-  return QNN_OK;
-}
-
-int qnn_maxpool_lut(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
-                    const uint8_t* dir, const float* vlut, float* out_f32, const int8_t* lut0,
-                    const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
-                    qnn_stream_t stream) {
-  QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
+int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
+                   const qnn_bn_params* bn, int relu, float* out_f32, int f32_tiled, const int8_t* lut0,
+                   const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                   qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && c > 0 && c % 16 == 0 && c <= 256 && k > 0 && stride > 0 && pad >= 0 &&
+                  2 * pad <= k,
+              "bad shape (c % 16 == 0, c <= 256, pad <= k/2)");
   QNN_REQUIRE(ho == (h + 2 * pad - k) / stride + 1 && wo == (w + 2 * pad - k) / stride + 1, "ho/wo inconsistent");
-  QNN_REQUIRE(dir && (((uintptr_t)dir) & 3) == 0, "dir must be non-null and 4-byte aligned");
-  QNN_REQUIRE(!out_f32 || vlut, "out_f32 needs vlut");
-  QNN_REQUIRE(!(code0 && code0->ptr) || lut0, "code0 needs lut0");
-  QNN_REQUIRE(!(code1 && code1->ptr) || lut1, "code1 needs lut1");
-  if (int rc = check_code(code0, c, "bad code0")) return rc;
-  if (int rc = check_code(code1, c, "bad code1")) return rc;
+  QNN_REQUIRE(bn && bn->mean && bn->sq && bn->wq && bn->bq && bn->scale > 0.f, "bad RangeBN params");
+  const bool has0 = code0 && code0->ptr, has1 = code1 && code1->ptr;
+  QNN_REQUIRE(!has0 || (lut0 && (((uintptr_t)lut0) & 15) == 0), "code0 needs a 16-B aligned lut0");
+  QNN_REQUIRE(!has1 || (lut1 && (((uintptr_t)lut1) & 15) == 0), "code1 needs a 16-B aligned lut1");
+  QNN_REQUIRE(out_f32 || has0 || has1, "no output");
+  QNN_REQUIRE(!out_f32 || (((uintptr_t)out_f32) & 15) == 0, "out_f32 must be 16-byte aligned");
+  auto code16 = [&](const qnn_code_out* o) {
+    return !o || !o->ptr || (o->cp >= c && o->cp % 16 == 0 && o->scale > 0.f && o->pad >= 0 &&
+                             (((uintptr_t)o->ptr) & 15) == 0);
+  };
+  QNN_REQUIRE(code16(code0) && code16(code1), "bad code output (cp % 16, 16-B aligned)");
   if (n == 0) return QNN_OK;
-  QNN_REQUIRE(q, "null input");
-  const qnn_code_out c0 = code0 ? *code0 : none_code(), c1 = code1 ? *code1 : none_code();
-  hipLaunchKernelGGL(maxpool_lut_kernel, dim3(grid_for((int64_t)n * ho * wo * (c / 4))), dim3(256), 0,
-                     (hipStream_t)stream, q, n, h, w, c, k, stride, pad, ho, wo, dir, vlut, out_f32, lut0, c0, lut1, c1);
-  QNN_LAUNCH_CHECK("qnn_maxpool_lut");
+  QNN_REQUIRE(q && (((uintptr_t)q) & 15) == 0, "q must be non-null and 16-byte aligned");
+  const qnn_code_out c0 = has0 ? *code0 : none_code();
+  const qnn_code_out c1 = has1 ? *code1 : none_code();
+  const int lds = c * 17 + ((has0 ? 1 : 0) + (has1 ? 1 : 0)) * c * 256 + 16;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)maxpool_bn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(maxpool_bn)");
+  const int64_t threads = cdiv((int64_t)n * ho * wo, 32) * (c / 16) * 32;
+  hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(threads)), dim3(256), lds, (hipStream_t)stream, q, n, h, w, c,
+                     k, stride, pad, ho, wo, *bn, relu, out_f32, f32_tiled, has0 ? lut0 : nullptr, c0,
+                     has1 ? lut1 : nullptr, c1);
+  QNN_LAUNCH_CHECK("qnn_maxpool_bn");
   return QNN_OK;
 }
 
@@ -259,8 +314,8 @@ int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out
   return QNN_OK;
 }
 
-int qnn_avgpool_quant(const float* x, int n, int hw, int c, float* out_f32, const qnn_code_out* code0,
-                      qnn_stream_t stream) {
+int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* out_f32,
+                      const qnn_code_out* code0, qnn_stream_t stream) {
   QNN_REQUIRE(n >= 0 && hw > 0 && c > 0 && c % 4 == 0, "bad shape");
   QNN_REQUIRE(out_f32 || (code0 && code0->ptr), "no output");
   if (int rc = check_code(code0, c, "bad code0")) return rc;
@@ -268,7 +323,7 @@ int qnn_avgpool_quant(const float* x, int n, int hw, int c, float* out_f32, cons
   QNN_REQUIRE(x, "null input");
   const qnn_code_out c0 = code0 ? *code0 : none_code();
   hipLaunchKernelGGL(avgpool_quant_kernel, dim3(grid_for((int64_t)n * (c / 4))), dim3(256), 0, (hipStream_t)stream, x,
-                     n, hw, c, out_f32, c0);
+                     n, hw, c, x_tiled, out_f32, c0);
   QNN_LAUNCH_CHECK("qnn_avgpool_quant");
   return QNN_OK;
 }

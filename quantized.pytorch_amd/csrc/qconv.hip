@@ -16,13 +16,22 @@
 //   border term: per (row class, col class, c) table staged in LDS.
 // Then either the drop-in output (fp32 NCHW, the reference module boundary), or
 // the fused chain of the model graph: RangeBN eval (quantize.py:461-499, exact
-// fp32 op order) -> + residual -> ReLU -> fp32 NHWC and/or requantized NHWC8
-// codes for up to two consumer convs (their QuantMeasure ranges).
+// fp32 op order) -> + residual -> ReLU -> fp32 (C-tile or NHWC) and/or requantized
+// NHWC8 codes for up to two consumer convs (their QuantMeasure ranges).
 //
 // Block: 256 threads = 4 waves, each wave a 64x64 tile (2x2 MFMA 32x32x32).
-// K stage = 128 bytes; two LDS stages filled by LDS-DMA, counted vmcnt, raw
-// s_barrier; rows XOR-swizzled so ds_read_b128 fragment reads are conflict-free.
+// K stage = BK (64 or 128) bytes; two LDS stages filled by LDS-DMA (counted vmcnt,
+// raw s_barrier), rows XOR-swizzled so ds_read_b128 fragment reads are
+// conflict-free; the stage loop is unrolled by two so every LDS address is a
+// per-lane constant plus an immediate, and fragments of k-step s+1 are read while
+// the MFMAs of step s run.  Gather addresses: the tap of each 16-byte chunk is
+// uniform per stage (or one of two) whenever Cp >= 8*BK/128, so its offset is
+// scalar arithmetic; only narrow-channel inputs use a per-lane LDS tap table.
+// Code stores: two v_permlane32_swap levels turn each lane's 4 dwords (channels
+// 8g+4h..) into 16 contiguous channels -> one 16-byte store per 32-channel group.
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "qnn_internal.h"
 
@@ -32,18 +41,50 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+#ifndef QNN_ABLATE
+#define QNN_ABLATE 0  // diagnostic builds only (make ablate): 1 no loads, 2 no MFMA, 3 no epilogue
+#endif
+
+#ifndef QNN_STAMP
+#define QNN_STAMP 0  // diagnostic builds only (make stamp): per-wave s_memtime phase sums
+#endif
+#if QNN_STAMP
+// [block][wave][10]: realtime start/end, cycles in prologue / issue / wait+barrier /
+// compute / trailing barrier / epilogue, HW_ID, stages
+__device__ unsigned long long qnn_dbg_stamps[1 << 20];
+__device__ unsigned long long qnn_dbg_epi[1 << 18];  // [block][wave][4]: staging, pixel state, body
+#define QNN_TSV(v)                                                                        \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+#define QNN_TS(v)                                                                         \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+#else
+#define QNN_TS(v) ((void)0)
+#define QNN_TSV(v) ((void)0)
+#endif
+
 constexpr int MAX_TAPS = 64;
 constexpr int MAX_CLASSES = 32;
 constexpr int MAX_MASK = 1024;
 constexpr int KPAD_ALIGN = 128;  // packed weight rows are multiples of 128 bytes (any BK divides)
 
+enum { TAP_ONE = 0, TAP_TWO = 1, TAP_LDS = 2 };
+
 struct Params {
   qnn_conv_desc d;
   qnn_epilogue e;
-  int M;        // n*ho*wo
-  int taps;     // kh*kw
-  int lgcpt;    // log2(cp/16)
-  int nstage;   // kpad / BK
+  int M;         // n*ho*wo
+  int taps;      // kh*kw
+  int lgcpt;     // log2(cp/16): 16-byte chunks per tap
+  int kw_magic;  // ceil(2^16 / kw): t / kw == (t * kw_magic) >> 16 for t < 64
+  int ct;        // C-tile columns, ceil(cout / 32)
 };
 
 // Byte offset of 16-byte chunk `chunk` of LDS row `row` (rows of BK bytes): XOR swizzle so
@@ -62,23 +103,90 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-__device__ __forceinline__ void store_code4(int8_t* p, float4 v, float nm, float s, float inv, float qmax) {
-  int b0 = (int)quant_code_fast(v.x, nm, s, inv, qmax) - 128;
-  int b1 = (int)quant_code_fast(v.y, nm, s, inv, qmax) - 128;
-  int b2 = (int)quant_code_fast(v.z, nm, s, inv, qmax) - 128;
-  int b3 = (int)quant_code_fast(v.w, nm, s, inv, qmax) - 128;
-  *reinterpret_cast<int*>(p) = (b0 & 255) | ((b1 & 255) << 8) | ((b2 & 255) << 16) | ((b3 & 255) << 24);
+// Byte offset of tap t (row-major over kh x kw) from a pixel's tap (0, 0); uniform.
+__device__ __forceinline__ int tap_offset(const Params& p, int t) {
+  const int r = (t * p.kw_magic) >> 16;
+  return (r * p.d.wp + (t - r * p.d.kw)) * p.d.cp;
 }
 
-// Epilogue shared by the implicit-GEMM and halo kernels.  sumq[j]: full receptive-field
-// sum of q'_x for this lane's pixel of column tile j.  smem: >= epilogue LDS bytes.
-template <int BM, bool FUSED>
+__device__ __forceinline__ int code_byte(float v, float nm, float s, float inv, float qmax) {
+  return ((int)quant_code_fast(v, nm, s, inv, qmax) - 128) & 255;
+}
+
+// Lane holds dwords g = 0..3 = channels [8g + 4h, 8g + 4h + 4) of a 32-channel group
+// (h = lane / 32).  Two half-exchange levels leave lanes 0-31 with channels 0-15 and
+// lanes 32-63 with channels 16-31 in order; returns them as one 16-byte vector.
+__device__ __forceinline__ v4i gather16(int d0, int d1, int d2, int d3) {
+  auto r01 = __builtin_amdgcn_permlane32_swap(d0, d1, false, false);
+  auto r23 = __builtin_amdgcn_permlane32_swap(d2, d3, false, false);
+  auto r02 = __builtin_amdgcn_permlane32_swap(r01[0], r23[0], false, false);
+  auto r13 = __builtin_amdgcn_permlane32_swap(r01[1], r23[1], false, false);
+  return (v4i){(int)r02[0], (int)r13[0], (int)r02[1], (int)r13[1]};
+}
+
+struct CodeDst {
+  int8_t* ptr;
+  int cp, pad, hp, wp;
+};
+
+__device__ __forceinline__ void store_codes(const CodeDst& t, int n, int ho, int wo, int ch, bool ok, v4i v) {
+  if (ok && ch < t.cp)
+    *reinterpret_cast<v4i*>(t.ptr + (((int64_t)n * t.hp + ho + t.pad) * t.wp + wo + t.pad) * t.cp + ch) = v;
+}
+
+// Epilogue kinds (one kernel instantiation each, so a kernel carries only its path):
+//   EK_NCHW   mode 0: the drop-in fp32 NCHW output of QConv2d / QLinear
+//   EK_LUT    conv -> RangeBN -> ReLU -> one consumer's codes via the per-channel table
+//   EK_BNCODE conv -> RangeBN input codes only (stem before the code-domain max-pool)
+//   EK_GEN    any other fused chain: [RangeBN] [+ residual] [ReLU] -> fp32 / codes x2
+enum { EK_NCHW = 0, EK_LUT = 1, EK_BNCODE = 2, EK_GEN = 3 };
+
+static inline int epi_kind(const qnn_epilogue& e) {
+  if (e.mode == 0) return EK_NCHW;
+  if (e.lut) return EK_LUT;
+  if (e.out_bncode && !e.out_f32 && !e.out_code0 && !e.out_code1) return EK_BNCODE;
+  return EK_GEN;
+}
+
+// Epilogue LDS bytes: params [7][BM] fp32, border table [nclass][BM] fp32, LUT [BM][256].
+static inline int epi_lds_bytes(const qnn_epilogue& e, int BM) {
+  return 4 * (7 + e.nclass) * BM + (epi_kind(e) == EK_LUT ? 256 * BM : 0);
+}
+
+// sumq[j]: full receptive-field sum of q'_x for this lane's pixel of column tile j.
+template <int BM, int EK>
 __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], const int (&sumq)[2], int8_t* smem,
-                                         int m0, int c0, int wm, int wn, int lane) {
+                                         int m0, int c0, int wm, int wn, int lane, int tid) {
   const qnn_conv_desc& d = p.d;
-  const int tid = threadIdx.x, frow = lane & 31, fh = lane >> 5;
-  const int HoWo = d.ho * d.wo;
   const qnn_epilogue& e = p.e;
+  const int frow = lane & 31, fh = lane >> 5;
+  const int HoWo = d.ho * d.wo;
+#if QNN_STAMP
+  unsigned long long e0 = 0, e1 = 0, e2 = 0, e3 = 0;
+#endif
+  QNN_TSV(e0);
+
+  // residual prefetch, 8 float4 (one 32-channel half) at a time: half 0 before the
+  // parameter staging, half 1 while half 0 is processed (each load would otherwise be
+  // a serialized HBM round trip)
+  float4 res[2][2][4];
+  const bool has_res = EK == EK_GEN && e.residual != nullptr;
+  auto load_res = [&](int i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int m = m0 + wn * 64 + j * 32 + frow;
+      if (m > p.M - 1) m = p.M - 1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int c = c0 + wm * 64 + i * 32 + 8 * g + 4 * fh;
+        if (c > d.cout - 4) c = d.cout - 4;
+        const int64_t fi = e.f32_tiled ? ctile_index(m, c, p.ct) : (int64_t)m * d.cout + c;
+        res[i][j][g] = *reinterpret_cast<const float4*>(e.residual + fi);
+      }
+    }
+  };
+  if (EK == EK_GEN && has_res) load_res(0);
+
   float* s_f = reinterpret_cast<float*>(smem);  // main-loop LDS is free now
   // [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq  [7BM..) table[cls][BM]
   const int nparam = 7 * BM;
@@ -88,7 +196,7 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
     s_f[i] = ok ? e.sxsw[c] : 0.f;
     s_f[BM + i] = ok ? e.sxbw[c] : 0.f;
     s_f[2 * BM + i] = (ok && e.bias) ? e.bias[c] : 0.f;
-    if (FUSED && e.bn_mean) {
+    if (EK != EK_NCHW && e.bn_mean) {
       s_f[3 * BM + i] = ok ? e.bn_mean[c] : 0.f;
       s_f[4 * BM + i] = ok ? e.bn_sq[c] : 0.f;
       s_f[5 * BM + i] = ok ? e.bn_wq[c] : 0.f;
@@ -99,16 +207,19 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
     const int cls = i / BM, c = c0 + (i - cls * BM);
     s_f[nparam + i] = c < d.cout ? e.table[cls * d.cout + c] : 0.f;
   }
-  int8_t* s_lut = smem + 4 * (7 + MAX_CLASSES) * BM;  // [BM][256] next-layer codes (FUSED && e.lut)
-  if (FUSED && e.lut) {
-    for (int i = tid; i < BM * 16; i += 256) {
+  int8_t* s_lut = smem + 4 * (7 + e.nclass) * BM;  // [BM][256] next-layer codes (EK_LUT)
+  if constexpr (EK == EK_LUT) {
+#pragma unroll
+    for (int k = 0; k < BM * 16 / 256; ++k) {
+      const int i = tid + 256 * k;
       const int c = c0 + (i >> 4);
-      if (c < d.cout)
-        *reinterpret_cast<v4i*>(s_lut + 16 * i) = *reinterpret_cast<const v4i*>(e.lut + (int64_t)c * 256 + 16 * (i & 15));
+      v4i v = {0, 0, 0, 0};
+      if (c < d.cout) v = *reinterpret_cast<const v4i*>(e.lut + (int64_t)c * 256 + 16 * (i & 15));
+      *reinterpret_cast<v4i*>(s_lut + 16 * i) = v;
     }
   }
   __syncthreads();
-  const float bn_inv = 1.0f / e.bn_scale, c0_inv = 1.0f / e.code0_scale, c1_inv = 1.0f / e.code1_scale;
+  QNN_TSV(e1);
 
   // per-pixel (lane) state for the two 32-pixel column tiles of this wave
   int pm[2], pn[2], phw[2], pho[2], pwo[2], ptab[2];
@@ -125,110 +236,151 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
     ptab[j] = nparam + (e.hcls[pho[j]] * e.nwc + e.wcls[pwo[j]]) * BM;
     psq[j] = (float)sumq[j];
   }
-  // channel groups outer (params loaded once), pixel tiles inner
+  QNN_TSV(e2);
+
+  if constexpr (EK == EK_NCHW) {
+    // drop-in output: NCHW fp32 (lanes = consecutive pixels of one channel plane)
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
-      const int c = c0 + cl;
-      if (FUSED && c >= d.cout) continue;  // cout % 4 == 0 in fused mode
-      float a_sxsw[4], a_sxbw[4], a_bias[4];
+      for (int g = 0; g < 4; ++g) {
+        const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;
+        const int c = c0 + cl;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a_sxsw[u] = s_f[cl + u];
-        a_sxbw[u] = s_f[BM + cl + u];
-        a_bias[u] = s_f[2 * BM + cl + u];
+        for (int j = 0; j < 2; ++j) {
+          if (pm[j] >= p.M) continue;
+          float* yp = e.out_f32 + ((int64_t)pn[j] * d.cout + c) * HoWo + phw[j];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float y = fmaf(s_f[cl + u], (float)acc[i][j][4 * g + u],
+                                 fmaf(s_f[BM + cl + u], psq[j], s_f[ptab[j] + cl + u]));
+            if (c + u < d.cout) yp[(int64_t)u * HoWo] = y + s_f[2 * BM + cl + u];
+          }
+        }
       }
+    }
+  } else {
+    const float bn_inv = 1.0f / e.bn_scale, c0_inv = 1.0f / e.code0_scale, c1_inv = 1.0f / e.code1_scale;
+    const CodeDst t0 = {e.out_code0, e.code0_cp, e.code0_pad, e.code0_hp, e.code0_wp};
+    const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
+    const CodeDst tb = {reinterpret_cast<int8_t*>(e.out_bncode), d.cout, 0, d.ho, d.wo};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (EK == EK_GEN && has_res && i == 0) load_res(1);
+      const int cb = c0 + wm * 64 + i * 32;  // first channel of this lane's 32-channel group
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        if (pm[j] >= p.M) continue;
-        const int m = pm[j], n = pn[j], hw = phw[j], ho = pho[j], wo = pwo[j];
-        float v[4];
+        const bool pok = pm[j] < p.M;
+        int k0[4], k1[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float y = fmaf(a_sxsw[u], (float)acc[i][j][4 * g + u], fmaf(a_sxbw[u], psq[j], s_f[ptab[j] + cl + u]));
-          v[u] = y + a_bias[u];
-        }
-        if (!FUSED) {
-          float* yp = e.out_f32 + ((int64_t)n * d.cout + c) * HoWo + hw;
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (c + u < d.cout) yp[(int64_t)u * HoWo] = v[u];
-          continue;
-        }
-        if (e.lut) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated per channel (exact)
-          int r = 0;
+        for (int g = 0; g < 4; ++g) {
+          const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
+          const int c = c0 + cl;
+          const bool cok = c < d.cout;  // cout % 16 == 0: a 4-channel group is all in or all out
+          float v[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
-            r |= ((int)(uint8_t)s_lut[(cl + u) * 256 + q]) << (8 * u);
+            const float y = fmaf(s_f[cl + u], (float)acc[i][j][4 * g + u],
+                                 fmaf(s_f[BM + cl + u], psq[j], s_f[ptab[j] + cl + u]));
+            v[u] = y + s_f[2 * BM + cl + u];
           }
-          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
-          *reinterpret_cast<int*>(e.out_code0 + a) = r;
-          continue;
-        }
-        if (e.bn_mean) {
+          k0[g] = k1[g] = 0;
+          if constexpr (EK == EK_LUT) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated (exact)
+            int r = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
+              r |= ((int)(uint8_t)s_lut[(cl + u) * 256 + q]) << (8 * u);
+            }
+            k0[g] = cok ? r : 0;
+            continue;
+          }
           int qb[4];
+          if (EK == EK_BNCODE || e.bn_mean) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            qb[u] = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN.quantize_input
-          if (e.out_bncode) {
-            *reinterpret_cast<int*>(e.out_bncode + (int64_t)m * d.cout + c) =
-                qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24);
-            if (!e.out_f32 && !e.out_code0) continue;  // stem before the code-domain max-pool
+            for (int u = 0; u < 4; ++u)
+              qb[u] = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN input
           }
+          if constexpr (EK == EK_BNCODE) {
+            k0[g] = cok ? (qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24)) : 0;
+            continue;
+          } else {
+            if (e.bn_mean) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int l = cl + u;
-            float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
-            o = o * s_f[4 * BM + l];                                                   // * q(scale)
-            o = o * s_f[5 * BM + l];                                                   // * q(weight)
-            v[u] = o + s_f[6 * BM + l];                                                // + q(bias)
+              for (int u = 0; u < 4; ++u) {
+                const int l = cl + u;
+                float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
+                o = o * s_f[4 * BM + l];                                                   // * q(scale)
+                o = o * s_f[5 * BM + l];                                                   // * q(weight)
+                v[u] = o + s_f[6 * BM + l];                                                // + q(bias)
+              }
+            }
+            float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
+            if (has_res) {
+              const float4 r4 = res[i][j][g];
+              o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
+            }
+            if (e.relu) {
+              o4.x = fmaxf(o4.x, 0.f); o4.y = fmaxf(o4.y, 0.f); o4.z = fmaxf(o4.z, 0.f); o4.w = fmaxf(o4.w, 0.f);
+            }
+            if (e.out_f32 && pok && cok) {
+              const int64_t fi = e.f32_tiled ? ctile_index(pm[j], c, p.ct) : (int64_t)pm[j] * d.cout + c;
+              *reinterpret_cast<float4*>(e.out_f32 + fi) = o4;
+            }
+            if (e.out_code0 && cok) {
+              const float nm = e.code0_neg_min, s = e.code0_scale, q = e.code0_qmax;
+              k0[g] = code_byte(o4.x, nm, s, c0_inv, q) | (code_byte(o4.y, nm, s, c0_inv, q) << 8) |
+                      (code_byte(o4.z, nm, s, c0_inv, q) << 16) | (code_byte(o4.w, nm, s, c0_inv, q) << 24);
+            }
+            if (e.out_code1 && cok) {
+              const float nm = e.code1_neg_min, s = e.code1_scale, q = e.code1_qmax;
+              k1[g] = code_byte(o4.x, nm, s, c1_inv, q) | (code_byte(o4.y, nm, s, c1_inv, q) << 8) |
+                      (code_byte(o4.z, nm, s, c1_inv, q) << 16) | (code_byte(o4.w, nm, s, c1_inv, q) << 24);
+            }
           }
         }
-        float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
-        if (e.residual) {
-          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + (int64_t)m * d.cout + c);
-          o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
-        }
-        if (e.relu) {
-          o4.x = fmaxf(o4.x, 0.f); o4.y = fmaxf(o4.y, 0.f); o4.z = fmaxf(o4.z, 0.f); o4.w = fmaxf(o4.w, 0.f);
-        }
-        if (e.out_f32) *reinterpret_cast<float4*>(e.out_f32 + (int64_t)m * d.cout + c) = o4;
-        if (e.out_code0) {
-          const int64_t a = (((int64_t)n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) * e.code0_cp + c;
-          store_code4(e.out_code0 + a, o4, e.code0_neg_min, e.code0_scale, c0_inv, e.code0_qmax);
-        }
-        if (e.out_code1) {
-          const int64_t a = (((int64_t)n * e.code1_hp + ho + e.code1_pad) * e.code1_wp + wo + e.code1_pad) * e.code1_cp + c;
-          store_code4(e.out_code1 + a, o4, e.code1_neg_min, e.code1_scale, c1_inv, e.code1_qmax);
+        const int ch = cb + 16 * fh;
+        if constexpr (EK == EK_BNCODE) {
+          store_codes(tb, pn[j], pho[j], pwo[j], ch, pok, gather16(k0[0], k0[1], k0[2], k0[3]));
+        } else {
+          if (EK == EK_LUT || e.out_code0)
+            store_codes(t0, pn[j], pho[j], pwo[j], ch, pok, gather16(k0[0], k0[1], k0[2], k0[3]));
+          if (EK == EK_GEN && e.out_code1)
+            store_codes(t1, pn[j], pho[j], pwo[j], ch, pok, gather16(k1[0], k1[1], k1[2], k1[3]));
         }
       }
     }
   }
+#if QNN_STAMP
+  QNN_TSV(e3);
+  if (lane == 0 && blockIdx.x < (1 << 18) / 16) {
+    unsigned long long* o = qnn_dbg_epi + ((size_t)blockIdx.x * 4 + (tid >> 6)) * 4;
+    o[0] = e1 - e0; o[1] = e2 - e1; o[2] = e3 - e2; o[3] = 0;
+  }
+#endif
 }
 
-template <int BM, int BN, int BK, bool FUSED, bool MASKED>
-__global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+template <int BM, int BN, int BK, int EK, int TAPM, bool MASKED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GEN ? 2 : 3))) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                     const Params p) {
   constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == 4, "4 waves of 64x64");
   static_assert(BK == 64 || BK == 128, "BK");
-  constexpr int CPR = BK / 16;    // 16-B chunks per LDS row
-  constexpr int RPI = 1024 / BK;  // rows per 1 KiB LDS-DMA wave-instruction
+  static_assert(!MASKED || TAPM == TAP_LDS, "masked (space-to-depth) stems use the LDS tap table");
+  constexpr int CPR = BK / 16;        // 16-B chunks per LDS row
+  constexpr int RPI = 1024 / BK;      // rows per 1 KiB LDS-DMA wave-instruction
   constexpr int NA = BM / (4 * RPI);  // glds per wave per stage for A
   constexpr int NB = BN / (4 * RPI);
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int MAIN = 2 * STAGE + 4 * MAX_TAPS + (MASKED ? MAX_MASK : 0);
-  constexpr int EPI = 4 * (7 + MAX_CLASSES) * BM + (FUSED ? 256 * BM : 0);  // params, border table, LUT
-  // one LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) int8_t smem[MAIN > EPI ? MAIN : EPI];
+  constexpr int KS = BK / 32;  // MFMA k-steps per stage
+  // one dynamic LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   int* s_tap = reinterpret_cast<int*>(smem + 2 * STAGE);
   int8_t* s_mask = smem + 2 * STAGE + 4 * MAX_TAPS;
 
   const qnn_conv_desc& d = p.d;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
 
   // ---- XCD-aware, bijective block -> tile map: each XCD gets a contiguous run of
@@ -245,46 +397,73 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
   const int c0 = (t % nby) * BM;
   const int HoWo = d.ho * d.wo;
 
-  if (tid < p.taps) s_tap[tid] = ((tid / d.kw) * d.wp + (tid % d.kw)) * d.cp;
+  if constexpr (TAPM == TAP_LDS) {
+    if (tid < p.taps) s_tap[tid] = ((tid / d.kw) * d.wp + (tid % d.kw)) * d.cp;
+  }
   if constexpr (MASKED) {
     for (int i = tid; i < d.kpad / 16; i += 256)
       *reinterpret_cast<v4i*>(s_mask + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
   }
 
-  // ---- per-lane load state
-  uint32_t boff[NB];
-  int bchunk[NB];
+  // ---- per-lane gather state: B chunk (row, slot) -> pixel base + chunk-in-tap offset,
+  // and which of the stage's taps the chunk belongs to
+  const int cpt_mask = (1 << p.lgcpt) - 1;
+  uint32_t bbase[NB];
+  int bdelta[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int row = RPI * (wave + 4 * j) + lane / CPR;
     int m = m0 + row;
     if (m > p.M - 1) m = p.M - 1;
     const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
-    boff[j] = (uint32_t)(((n * d.hp + ho * d.sh) * d.wp + wo * d.sw) * d.cp);
-    bchunk[j] = (swz<BK>(row, lane % CPR) - row * BK) >> 4;  // the chunk that lands in this lane's slot
+    const int bch = (swz<BK>(row, lane % CPR) - row * BK) >> 4;  // the chunk that lands in this lane's slot
+    bbase[j] = (uint32_t)(((n * d.hp + ho * d.sh) * d.wp + wo * d.sw) * d.cp) + ((bch & cpt_mask) << 4);
+    bdelta[j] = bch >> p.lgcpt;
   }
-  const int8_t* aptr[NA];
+  const int8_t* wblk = w + (int64_t)c0 * d.kpad;
+  uint32_t aoff[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const int row = RPI * (wave + 4 * j) + lane / CPR;
-    aptr[j] = w + (int64_t)(c0 + row) * d.kpad + (swz<BK>(row, lane % CPR) - row * BK);
+    aoff[j] = (uint32_t)(row * d.kpad + (swz<BK>(row, lane % CPR) - row * BK));
   }
-  const int cpt_mask = (1 << p.lgcpt) - 1;
-  __syncthreads();  // s_tap
+  if constexpr (TAPM == TAP_LDS || MASKED) __syncthreads();  // s_tap / s_mask
 
   auto issue = [&](int st, int buf) {
+    if (QNN_ABLATE == 1) return;
     int8_t* sa = smem + buf * STAGE;
     int8_t* sb = sa + BM * BK;
 #pragma unroll
-    for (int j = 0; j < NA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(aptr[j] + st * BK),
-                                       (lds_ptr_t)(sa + (wave + 4 * j) * 1024), 16, 0, 0);
+    for (int j = 0; j < NA; ++j) {
+      uint32_t off = aoff[j] + (uint32_t)(st * BK);
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(sa + (wave + 4 * j) * 1024), 16, 0, 0);
+    }
+    const int t0 = (st * CPR) >> p.lgcpt;                       // first tap of this stage
+    const uint32_t uin = (uint32_t)(((st * CPR) & cpt_mask) << 4);  // chunk-in-tap part (cp > 16*CPR)
+    const uint32_t zoff = (uint32_t)d.zero_off;
+    uint32_t T0 = 0, T1 = 0;
+    bool v0 = false, v1 = false;
+    if constexpr (TAPM != TAP_LDS) {
+      v0 = t0 < p.taps;
+      T0 = (uint32_t)tap_offset(p, t0) + uin;
+      if constexpr (TAPM == TAP_TWO) {
+        v1 = t0 + 1 < p.taps;
+        T1 = (uint32_t)tap_offset(p, t0 + 1);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int kc = st * CPR + bchunk[j];
-      const int tap = kc >> p.lgcpt;
-      uint32_t off = tap < p.taps ? boff[j] + (uint32_t)s_tap[tap] + (uint32_t)((kc & cpt_mask) << 4)
-                                  : (uint32_t)d.zero_off;
+      uint32_t off;
+      if constexpr (TAPM == TAP_ONE) {
+        off = v0 ? bbase[j] + T0 : zoff;
+      } else if constexpr (TAPM == TAP_TWO) {
+        off = bdelta[j] ? (v1 ? bbase[j] + T1 : zoff) : (v0 ? bbase[j] + T0 : zoff);
+      } else {
+        const int tap = t0 + bdelta[j];
+        const uint32_t to = (uint32_t)s_tap[tap < MAX_TAPS ? tap : MAX_TAPS - 1];
+        off = tap < p.taps ? bbase[j] + uin + to : zoff;
+      }
       asm volatile("" : "+v"(off));  // keep ONE per-lane-address load (no saddr/vaddr branch split)
       __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wave + 4 * j) * 1024), 16, 0, 0);
     }
@@ -297,309 +476,190 @@ __global__ __launch_bounds__(256) void qconv_kernel(const int8_t* __restrict__ x
     for (int j = 0; j < 2; ++j) acc[i][j] = (v16i){0};
   int sumq[2] = {0, 0};
 
+  // per-lane fragment offsets of each k-step (the XOR swizzle depends only on frow)
   const int frow = lane & 31, fh = lane >> 5;
-  issue(0, 0);
-  const int nstage = p.d.kpad / BK;
-  for (int st = 0; st < nstage; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nstage) {
-      issue(st + 1, buf ^ 1);
-      wait_vmcnt<NA + NB>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    const int8_t* sa = smem + buf * STAGE;
-    const int8_t* sb = sa + BM * BK;
+  int offa[KS], offb[KS];
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int chunk = 2 * ks + fh;
-      v4i fa[2], fb[2];
+  for (int ks = 0; ks < KS; ++ks) {
+    const int xo = swz<BK>(frow, 2 * ks + fh) - frow * BK;
+    offa[ks] = (wm * 64 + frow) * BK + xo;
+    offb[ks] = BM * BK + (wn * 64 + frow) * BK + xo;
+  }
+
+  auto compute = [&](auto bufc, int st) {
+    constexpr int BO = decltype(bufc)::value * STAGE;
+    v4i fa[2][2], fb[2][2];
+    auto load = [&](int ks, int slot) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz<BK>(wm * 64 + i * 32 + frow, chunk));
+      for (int i = 0; i < 2; ++i) fa[slot][i] = *reinterpret_cast<const v4i*>(smem + BO + offa[ks] + i * 32 * BK);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[slot][j] = *reinterpret_cast<const v4i*>(smem + BO + offb[ks] + j * 32 * BK);
+    };
+    load(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < KS) load(ks + 1, cur ^ 1);
+      v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
+      if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(s_mask + st * BK + 16 * (2 * ks + fh));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        fb[j] = *reinterpret_cast<const v4i*>(sb + swz<BK>(wn * 64 + j * 32 + frow, chunk));
-        v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
-        if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(s_mask + st * BK + 16 * chunk);
-        int s = __builtin_amdgcn_sdot4(fb[j].x, ones.x, sumq[j], false);
-        s = __builtin_amdgcn_sdot4(fb[j].y, ones.y, s, false);
-        s = __builtin_amdgcn_sdot4(fb[j].z, ones.z, s, false);
-        sumq[j] = __builtin_amdgcn_sdot4(fb[j].w, ones.w, s, false);
+        int s = __builtin_amdgcn_sdot4(fb[cur][j].x, ones.x, sumq[j], false);
+        s = __builtin_amdgcn_sdot4(fb[cur][j].y, ones.y, s, false);
+        s = __builtin_amdgcn_sdot4(fb[cur][j].z, ones.z, s, false);
+        sumq[j] = __builtin_amdgcn_sdot4(fb[cur][j].w, ones.w, s, false);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          if (QNN_ABLATE == 2) {
+            asm volatile("" ::"v"(fa[cur][i]), "v"(fb[cur][j]));
+            acc[i][j][0] += fa[cur][i].x;
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+  };
+
+  const int nstage = d.kpad / BK;
+#if QNN_STAMP
+  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, c_iss = 0, c_wait = 0, c_comp = 0, c_bar = 0;
+  const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
+  issue(0, 0);
+  auto step = [&](auto bufc, int st) {
+    constexpr int b = decltype(bufc)::value;
+    QNN_TS(ts0);
+    if (st + 1 < nstage) {
+      issue(st + 1, b ^ 1);
+      QNN_TS(ts1);
+      wait_vmcnt<NA + NB>();
+    } else {
+      QNN_TS(ts1);
+      wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+    QNN_TS(ts2);
+    compute(bufc, st);
+    QNN_TS(ts3);
+    __builtin_amdgcn_s_barrier();
+    QNN_TS(ts4);
+#if QNN_STAMP
+    c_iss += ts1 - ts0;
+    c_wait += ts2 - ts1;
+    c_comp += ts3 - ts2;
+    c_bar += ts4 - ts3;
+#endif
+  };
+#if QNN_STAMP
+  QNN_TS(ts0);
+  const unsigned long long c_pro = ts0 - t_begin;
+#endif
+  for (int st = 0; st < nstage; st += 2) {
+    step(std::integral_constant<int, 0>{}, st);
+    if (st + 1 < nstage) step(std::integral_constant<int, 1>{}, st + 1);
   }
 
-  // ================================================================ epilogue
 #pragma unroll
   for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
   __syncthreads();  // main-loop LDS is reused by the epilogue
-  epilogue<BM, FUSED>(p, acc, sumq, smem, m0, c0, wm, wn, lane);
+  if (QNN_ABLATE == 3) {
+    int z = sumq[0];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z ^= acc[i][j][r];
+    if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;  // keeps every MFMA live, (almost) never stores
+    return;
+  }
+#if QNN_STAMP
+  QNN_TS(ts0);
+#endif
+  epilogue<BM, EK>(p, acc, sumq, smem, m0, c0, wm, wn, lane, tid);
+#if QNN_STAMP
+  QNN_TS(ts1);
+  const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  unsigned hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  if (lane == 0 && blockIdx.x < (1 << 20) / 40) {
+    unsigned long long* o = qnn_dbg_stamps + ((size_t)blockIdx.x * 4 + wave) * 10;
+    o[0] = rt_start; o[1] = rt_end; o[2] = c_pro; o[3] = c_iss; o[4] = c_wait; o[5] = c_comp; o[6] = c_bar;
+    o[7] = ts1 - ts0; o[8] = hwid; o[9] = nstage;
+  }
+#endif
 }
 
-// ============================================================================ halo kernel
-// For kh x kw convs with Cp >= 32 (the ResNet 3x3s).  The implicit-GEMM kernel above
-// re-gathers every activation byte once per tap (9x for 3x3) through L1, which caps
-// it at the per-CU load bandwidth.  Here a block loads, per channel chunk of CK bytes,
-// the BAND of padded input rows covering its pixel tile's receptive field into LDS
-// ONCE (rows [n0*hp + ho0*sh, n1*hp + ho1*sh + kh - 1] of the flattened padded
-// buffer, every column, CK channels), then serves all kh*kw taps' B fragments from
-// it; only the per-tap weight slice [BM][CK] streams (LDS-DMA, double-buffered).
-// sum_valid(q'_x) comes from per-band-pixel channel sums S[q] (one v_dot4 pass per
-// band pixel instead of one per fragment), summed over the taps of each pixel.
-constexpr int MAX_BAND = 40960;
-
-template <int CPR>
-__device__ __forceinline__ int swz_c(int idx, int chunk) {
-  // chunk slot of 16-B chunk `chunk` in LDS row `idx` (rows of 16*CPR bytes): conflict-free
-  // ds_read_b128 over 16 consecutive rows
-  return chunk ^ ((idx / (16 / CPR)) & (CPR - 1));
+template <int BM, int BN, int BK>
+static int main_lds_bytes(int tapm, bool masked) {
+  return 2 * (BM + BN) * BK + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
 }
 
-template <int BM, int BN, int CK, bool FUSED>
-__global__ __launch_bounds__(256) void qconv_halo_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
-                                                         const Params p) {
-  constexpr int WM = BM / 64, WN = BN / 64;
-  static_assert(WM * WN == 4, "4 waves of 64x64");
-  constexpr int CPR = CK / 16;
-  constexpr int A_BYTES = BM * CK;
-  constexpr int NPA = A_BYTES / 1024;  // 1-KiB LDS-DMA pieces per weight slice
-  static_assert(NPA % 4 == 0, "every wave issues the same number of weight pieces");
-  constexpr int BAND_PIX = MAX_BAND / CK;
-  constexpr int OFF_S = MAX_BAND + 1024;            // band + slack for a partial last piece
-  constexpr int OFF_A = OFF_S + 4 * BAND_PIX;
-  constexpr int MAIN = OFF_A + 2 * A_BYTES;
-  constexpr int EPI = 4 * (7 + MAX_CLASSES) * BM + (FUSED ? 256 * BM : 0);
-  __shared__ __attribute__((aligned(16))) int8_t smem[MAIN > EPI ? MAIN : EPI];
-  int8_t* s_band = smem;
-  int* s_sum = reinterpret_cast<int*>(smem + OFF_S);
-  int8_t* s_a = smem + OFF_A;
-
-  const qnn_conv_desc& d = p.d;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int frow = lane & 31, fh = lane >> 5;
-
-  const int nby = (d.cout + BM - 1) / BM;
-  const int nblk = ((p.M + BN - 1) / BN) * nby;
-  int t;
-  {
-    const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
-    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  }
-  const int m0 = (t / nby) * BN;
-  const int c0 = (t % nby) * BM;
-  const int HoWo = d.ho * d.wo;
-
-  // band rows of this pixel tile (flattened padded rows n*hp + row)
-  int rlo, rhi;
-  {
-    const int mA = m0, mB = min(m0 + BN, p.M) - 1;
-    const int nA = mA / HoWo, hoA = (mA - nA * HoWo) / d.wo;
-    const int nB = mB / HoWo, hoB = (mB - nB * HoWo) / d.wo;
-    rlo = nA * d.hp + hoA * d.sh;
-    rhi = nB * d.hp + hoB * d.sh + d.kh - 1;
-  }
-  const int band_pix = (rhi - rlo + 1) * d.wp;
-  const int band_pieces = (band_pix * CK + 1023) >> 10;
-  const int8_t* xband = x + (int64_t)rlo * d.wp * d.cp;
-
-  // per-lane band pixel of tap (0,0) for the two 32-pixel column tiles
-  int P[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    int m = m0 + wn * 64 + j * 32 + frow;
-    if (m > p.M - 1) m = p.M - 1;
-    const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
-    P[j] = (n * d.hp + ho * d.sh - rlo) * d.wp + wo * d.sw;
-  }
-  // per-lane A fragment row offsets (fixed)
-  int arow[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) arow[i] = wm * 64 + i * 32 + frow;
-
-  const int taps = p.taps;
-  const int nch = d.cp / CK;
-  const int nsteps = nch * taps;
-
-  auto issue_a = [&](int step, int buf) {
-    const int ch = step / taps, tp = step - ch * taps;
-    const int8_t* src = w + (int64_t)c0 * d.kpad + tp * d.cp + ch * CK;
-#pragma unroll
-    for (int k = 0; k < NPA / 4; ++k) {
-      const int pc = wave + 4 * k;
-      const int L = pc * 64 + lane, row = L / CPR, slot = L % CPR;
-      __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)row * d.kpad + 16 * swz_c<CPR>(row, slot)),
-                                       (lds_ptr_t)(s_a + buf * A_BYTES + pc * 1024), 16, 0, 0);
-    }
-  };
-  auto issue_band = [&](int ch) {
-    const int8_t* src = xband + ch * CK;
-    for (int pc = wave; pc < band_pieces; pc += 4) {
-      const int L = pc * 64 + lane, q = L / CPR, slot = L % CPR;
-      uint32_t off = q < band_pix ? (uint32_t)(q * d.cp + 16 * swz_c<CPR>(q, slot))
-                                  : (uint32_t)(d.zero_off - (int64_t)rlo * d.wp * d.cp - ch * CK);
-      asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((const void*)(src + off), (lds_ptr_t)(s_band + pc * 1024), 16, 0, 0);
-    }
-  };
-
-  v16i acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (v16i){0};
-  int sumq[2] = {0, 0};
-
-  issue_a(0, 0);
-  for (int ch = 0; ch < nch; ++ch) {
-    issue_band(ch);
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    // per-band-pixel channel sums of the codes (exact)
-    for (int q = tid; q < band_pix; q += 256) {
-      int ssum = 0;
-#pragma unroll
-      for (int c = 0; c < CPR; ++c) {
-        const v4i v = *reinterpret_cast<const v4i*>(s_band + q * CK + 16 * c);
-        ssum = __builtin_amdgcn_sdot4(v.x, 0x01010101, ssum, false);
-        ssum = __builtin_amdgcn_sdot4(v.y, 0x01010101, ssum, false);
-        ssum = __builtin_amdgcn_sdot4(v.z, 0x01010101, ssum, false);
-        ssum = __builtin_amdgcn_sdot4(v.w, 0x01010101, ssum, false);
-      }
-      s_sum[q] = ssum;
-    }
-    __syncthreads();
-    for (int tp = 0; tp < taps; ++tp) {
-      const int step = ch * taps + tp;
-      const int buf = step & 1;
-      if (step + 1 < nsteps) {
-        issue_a(step + 1, buf ^ 1);
-        wait_vmcnt<NPA / 4>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      const int r = tp / d.kw, sx = tp - r * d.kw;
-      const int toff = r * d.wp + sx;
-      const int8_t* sa = s_a + buf * A_BYTES;
-      int bidx[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        bidx[j] = P[j] + toff;
-        sumq[j] += s_sum[bidx[j]];
-      }
-#pragma unroll
-      for (int ks = 0; ks < CK / 32; ++ks) {
-        const int chunk = 2 * ks + fh;
-        v4i fa[2], fb[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          fa[i] = *reinterpret_cast<const v4i*>(sa + arow[i] * CK + 16 * swz_c<CPR>(arow[i], chunk));
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          fb[j] = *reinterpret_cast<const v4i*>(s_band + bidx[j] * CK + 16 * swz_c<CPR>(bidx[j], chunk));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  __syncthreads();
-  epilogue<BM, FUSED>(p, acc, sumq, smem, m0, c0, wm, wn, lane);
-}
-
-// Largest band (bytes per channel byte) over the pixel tiles of one launch.
-static int64_t max_band_rows(const Params& p, int BN) {
-  const qnn_conv_desc& d = p.d;
-  const int HoWo = d.ho * d.wo;
-  int64_t worst = 0;
-  for (int m0 = 0; m0 < p.M; m0 += BN) {
-    const int mB = (m0 + BN < p.M ? m0 + BN : p.M) - 1;
-    const int nA = m0 / HoWo, hoA = (m0 - nA * HoWo) / d.wo;
-    const int nB = mB / HoWo, hoB = (mB - nB * HoWo) / d.wo;
-    const int64_t rows = (int64_t)(nB * d.hp + hoB * d.sh + d.kh - 1) - (nA * d.hp + hoA * d.sh) + 1;
-    if (rows > worst) worst = rows;
-  }
-  return worst;
-}
-
-template <int BM, int BN, int CK, bool FUSED>
-static void launch_halo(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+template <int BM, int BN, int BK, int EK, int TAPM, bool MASKED>
+static int launch_kernel(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  auto kern = qconv_kernel<BM, BN, BK, EK, TAPM, MASKED>;
+  static const hipError_t attr =  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  const int lds_main = main_lds_bytes<BM, BN, BK>(TAPM, MASKED);
+  const int lds_epi = epi_lds_bytes(p.e, BM);
+  const int lds = lds_main > lds_epi ? lds_main : lds_epi;
   const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
-  hipLaunchKernelGGL((qconv_halo_kernel<BM, BN, CK, FUSED>), dim3(nblk), dim3(256), 0, s, x, w, p);
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), lds, s, x, w, p);
+  return QNN_OK;
 }
 
-// Picks the halo kernel's channel chunk (0 = not applicable).  QNN_HALO=0 disables it.
-static int pick_halo_ck(const Params& p, int BM, int BN) {
-  static int enabled = [] {
-    const char* v = getenv("QNN_HALO");
-    return v ? atoi(v) : 1;
-  }();
-  const qnn_conv_desc& d = p.d;
-  if (!enabled || d.kmask || d.kh * d.kw < 2 || d.cp < 32) return 0;
-  const int64_t rows = max_band_rows(p, BN);
-  for (int ck : {128, 64, 32}) {
-    if (d.cp % ck) continue;
-    if ((BM * ck / 1024) % 4) continue;
-    if (rows * d.wp * ck <= MAX_BAND) return ck;
-  }
-  return 0;
+template <int BM, int BN, int BK, int EK>
+static int launch_tap(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  constexpr int CPR = BK / 16;
+  const int cpt = 1 << p.lgcpt;
+  if (p.d.kmask) return launch_kernel<BM, BN, BK, EK, TAP_LDS, true>(x, w, p, s);
+  if (cpt >= CPR) return launch_kernel<BM, BN, BK, EK, TAP_ONE, false>(x, w, p, s);
+  if (2 * cpt == CPR) return launch_kernel<BM, BN, BK, EK, TAP_TWO, false>(x, w, p, s);
+  return launch_kernel<BM, BN, BK, EK, TAP_LDS, false>(x, w, p, s);
 }
 
-template <int BM, int BN, bool FUSED>
-static bool try_halo(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  switch (pick_halo_ck(p, BM, BN)) {
-    case 128: launch_halo<BM, BN, 128, FUSED>(x, w, p, s); return true;
-    case 64: launch_halo<BM, BN, 64, FUSED>(x, w, p, s); return true;
-    case 32:
-      if constexpr (BM == 128) {
-        launch_halo<BM, BN, 32, FUSED>(x, w, p, s);
-        return true;
-      }
-      return false;
-    default: return false;
+template <int BM, int BN, int BK>
+static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  switch (epi_kind(p.e)) {
+    case EK_NCHW: return launch_tap<BM, BN, BK, EK_NCHW>(x, w, p, s);
+    case EK_LUT: return launch_tap<BM, BN, BK, EK_LUT>(x, w, p, s);
+    case EK_BNCODE: return launch_tap<BM, BN, BK, EK_BNCODE>(x, w, p, s);
+    default: return launch_tap<BM, BN, BK, EK_GEN>(x, w, p, s);
   }
 }
 
-template <int BM, int BN, int BK, bool FUSED>
-static void launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
-  if (p.d.kmask)
-    hipLaunchKernelGGL((qconv_kernel<BM, BN, BK, FUSED, true>), dim3(nblk), dim3(256), 0, s, x, w, p);
-  else
-    hipLaunchKernelGGL((qconv_kernel<BM, BN, BK, FUSED, false>), dim3(nblk), dim3(256), 0, s, x, w, p);
-}
-
-// K-stage depth: 64-byte stages halve the LDS of a block (more blocks per CU to hide
-// DMA latency and overlap one block's epilogue with another's MFMAs).  QNN_CONV_BK
-// overrides (64 / 128) for A/B measurements.
+// K-stage depth.  QNN_CONV_BK overrides (64 / 128) for A/B measurements.
 static int pick_bk(const Params& p) {
   static int forced = [] {
     const char* v = getenv("QNN_CONV_BK");
     return v ? atoi(v) : 0;
   }();
   if (forced == 64 || forced == 128) return forced;
-  return p.d.cout <= 64 ? 64 : 128;  // measured: BK=64 wins on 64-channel layers, 128 on wider
-}
-
-template <int BM, int BN, bool FUSED>
-static void launch_bk(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  if (try_halo<BM, BN, FUSED>(x, w, p, s)) return;
-  if (pick_bk(p) == 128) launch<BM, BN, 128, FUSED>(x, w, p, s);
-  else launch<BM, BN, 64, FUSED>(x, w, p, s);
+  return p.d.cout <= 64 ? 64 : 128;
 }
 
 }  // namespace qnn
 
 using namespace qnn;
+
+#if QNN_STAMP
+extern "C" int qnn_debug_stamps(void* dst, size_t bytes) {
+  if (bytes > sizeof(qnn_dbg_stamps)) bytes = sizeof(qnn_dbg_stamps);
+  return hip_check(hipMemcpyFromSymbol(dst, HIP_SYMBOL(qnn_dbg_stamps), bytes), "stamps");
+}
+extern "C" int qnn_debug_epi(void* dst, size_t bytes) {
+  if (bytes > sizeof(qnn_dbg_epi)) bytes = sizeof(qnn_dbg_epi);
+  return hip_check(hipMemcpyFromSymbol(dst, HIP_SYMBOL(qnn_dbg_epi), bytes), "stamps");
+}
+#endif
 
 extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
                                qnn_stream_t stream) {
@@ -609,7 +669,7 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   QNN_REQUIRE(d.n >= 0 && d.hp > 0 && d.wp > 0 && d.cout > 0 && d.kh > 0 && d.kw > 0 && d.sh > 0 && d.sw > 0,
               "bad shape");
   QNN_REQUIRE(d.cp >= 16 && (d.cp & (d.cp - 1)) == 0, "cp must be 16 * 2^j");
-  QNN_REQUIRE(d.kh * d.kw <= MAX_TAPS, "at most 64 taps");
+  QNN_REQUIRE(d.kh * d.kw <= MAX_TAPS && d.kw <= 64, "at most 64 taps");
   QNN_REQUIRE(d.ho > 0 && d.wo > 0 && (d.ho - 1) * d.sh + d.kh <= d.hp && (d.wo - 1) * d.sw + d.kw <= d.wp,
               "ho/wo exceed the padded input");
   QNN_REQUIRE(d.kpad % KPAD_ALIGN == 0 && d.kpad >= d.kh * d.kw * d.cp, "kpad must be a multiple of 128 covering K");
@@ -624,14 +684,20 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   if (e.mode == 0) {
     QNN_REQUIRE(e.out_f32 != nullptr, "mode 0 needs out_f32");
   } else {
-    QNN_REQUIRE(d.cout % 4 == 0, "fused mode needs cout % 4 == 0");
+    QNN_REQUIRE(d.cout % 16 == 0, "fused mode needs cout % 16 == 0");
     QNN_REQUIRE(!e.bn_mean || (e.bn_sq && e.bn_wq && e.bn_bq && e.bn_scale > 0.f), "incomplete RangeBN");
-    QNN_REQUIRE(!e.out_code0 || (e.code0_cp % 4 == 0 && e.code0_scale > 0.f), "bad code0");
-    QNN_REQUIRE(!e.out_code1 || (e.code1_cp % 4 == 0 && e.code1_scale > 0.f), "bad code1");
+    auto code_ok = [](const int8_t* ptr, int cp, float scale) {
+      return cp % 16 == 0 && scale > 0.f && (((uintptr_t)ptr) & 15) == 0;
+    };
+    QNN_REQUIRE(!e.out_code0 || code_ok(e.out_code0, e.code0_cp, e.code0_scale), "bad code0 (cp % 16, 16-B aligned)");
+    QNN_REQUIRE(!e.out_code1 || code_ok(e.out_code1, e.code1_cp, e.code1_scale), "bad code1 (cp % 16, 16-B aligned)");
+    QNN_REQUIRE(!e.out_bncode || (e.bn_mean && (((uintptr_t)e.out_bncode) & 15) == 0), "bncode needs RangeBN, 16-B aligned");
     QNN_REQUIRE(e.out_f32 || e.out_code0 || e.out_code1 || e.out_bncode, "fused mode without an output");
     QNN_REQUIRE(!e.lut || (e.bn_mean && e.out_code0 && !e.residual && !e.out_f32 && !e.out_code1 && !e.out_bncode &&
                            (((uintptr_t)e.lut) & 15) == 0),
                 "lut needs RangeBN, exactly one code output, no residual/fp32/bncode, 16-B aligned");
+    QNN_REQUIRE(!e.f32_tiled || ((((uintptr_t)e.out_f32) & 15) == 0 && (((uintptr_t)e.residual) & 15) == 0),
+                "C-tile fp32 maps must be 16-byte aligned");
   }
   Params p;
   p.d = d;
@@ -641,17 +707,15 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   p.M = (int)M;
   p.taps = d.kh * d.kw;
   p.lgcpt = __builtin_ctz(d.cp / 16);
-  p.nstage = 0;
+  p.kw_magic = (65536 + d.kw - 1) / d.kw;
+  p.ct = (int)cdiv(d.cout, 32);
   hipStream_t s = (hipStream_t)stream;
   const bool narrow = d.cout <= 64;
   QNN_REQUIRE(d.cout_pad >= (narrow ? 64 : 128) * (int)cdiv(d.cout, narrow ? 64 : 128), "cout_pad too small");
-  if (e.mode == 0) {
-    if (narrow) launch_bk<64, 256, false>(x, wq, p, s);
-    else launch_bk<128, 128, false>(x, wq, p, s);
-  } else {
-    if (narrow) launch_bk<64, 256, true>(x, wq, p, s);
-    else launch_bk<128, 128, true>(x, wq, p, s);
-  }
+  int rc;
+  if (narrow) rc = launch_ek<64, 256, 64>(x, wq, p, s);  // measured: BK=64 on 64-channel layers
+  else rc = pick_bk(p) == 128 ? launch_ek<128, 128, 128>(x, wq, p, s) : launch_ek<128, 128, 64>(x, wq, p, s);
+  if (rc != QNN_OK) return rc;
   QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
   return QNN_OK;
 }

@@ -39,16 +39,19 @@ __device__ __forceinline__ float quant_code(float x, float neg_min, float scale,
 }
 
 // quant_code without a per-element IEEE division, bit-identical to quant_code:
-// u = t * inv_scale (inv_scale = fl(1/scale)) is within 1.5 ulp of fl(t/scale), i.e.
-// |u - u*| < 2^-14 for |u| <= 256.  rint(clamp(.)) can differ from the exact one only
-// if a half-integer lies between u and u*, which forces |u - rint(u)| > 0.5 - 2^-14;
-// every such lane (and exact ties) takes the exact division (about 0.2 % of lanes).
+// with inv_scale = RN(1/scale) (the caller's correctly rounded 1.0f / scale) and
+// q0 = RN(t * inv_scale) within 1 ulp of t/scale, the exact remainder r = t - q0*scale
+// (one fma) and q = RN(q0 + r*inv_scale) give the correctly rounded quotient RN(t/scale)
+// (Markstein's theorem; checked against IEEE division on 4e8 pairs concentrated at
+// half-integer quotients, tests/test_quant_math.py).  Branch-free: 5 VALU.  Quotients
+// beyond 2^20 (and inf) take q0: they clamp to 0 or qmax whatever their last bit.
 __device__ __forceinline__ float quant_code_fast(float x, float neg_min, float scale, float inv_scale, float qmax) {
   const float t = x + neg_min;
-  const float uc = fminf(fmaxf(t * inv_scale, 0.0f), qmax);
-  const float r = rintf(uc);
-  if (fabsf(uc - r) > 0.4990234375f) return quant_code(x, neg_min, scale, qmax);
-  return r;
+  const float q0 = t * inv_scale;
+  const float r = fmaf(-q0, scale, t);
+  float q = fmaf(r, inv_scale, q0);
+  q = fabsf(q0) < 1048576.0f ? q : q0;
+  return rintf(fminf(fmaxf(q, 0.0f), qmax));
 }
 
 __device__ __forceinline__ float dequant(float q, float scale, float min) {
@@ -75,6 +78,12 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Element (m, c) of an fp32 [M][C] map in the C-tile layout (include/qnn.h, qnn_epilogue):
+// the MFMA 32x32 accumulator image, ct = ceil(C / 32) tile columns.
+__device__ __forceinline__ int64_t ctile_index(int64_t m, int c, int ct) {
+  return ((((m >> 5) * ct + (c >> 5)) * 4 + ((c & 31) >> 3)) << 8) + (((m & 31) + ((c & 4) << 3)) << 2) + (c & 3);
 }
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -14,9 +14,9 @@ import os
 import torch  # noqa: F401  (binds the process HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqnn_hip.so")
+LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -38,7 +38,7 @@ class Epilogue(ctypes.Structure):
                 ("code0_wp", c_int), ("code0_neg_min", c_float), ("code0_scale", c_float), ("code0_qmax", c_float),
                 ("out_code1", c_ptr), ("code1_cp", c_int), ("code1_pad", c_int), ("code1_hp", c_int),
                 ("code1_wp", c_int), ("code1_neg_min", c_float), ("code1_scale", c_float), ("code1_qmax", c_float),
-                ("lut", c_ptr)]
+                ("lut", c_ptr), ("f32_tiled", c_int)]
 
 class BnParams(ctypes.Structure):
     """qnn_bn_params (include/qnn.h)."""
@@ -69,12 +69,11 @@ SIGNATURES = {
     "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
-    "qnn_bn_value_lut": [_PB, c_int, c_int, c_ptr, c_ptr, c_ptr],
-    "qnn_maxpool_lut": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr,
-                        c_ptr, _PC, c_ptr, _PC, c_ptr],
+    "qnn_maxpool_bn": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,
+                       c_int, c_ptr, _PC, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
-    "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
+    "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],
     "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr, c_int, c_ptr],

@@ -42,6 +42,18 @@ def _f32(v):
     return float(np.float32(v))
 
 
+def ctile_numel(M, C):
+    """Floats of an fp32 [M][C] map in the C-tile layout (include/qnn.h, qnn_epilogue)."""
+    return -(-M // 32) * 32 * -(-C // 32) * 32
+
+
+def untile(buf, M, C):
+    """C-tile fp32 map -> row-major [M][C] (a copy; for tests and inspection)."""
+    mt, ct = -(-M // 32), -(-C // 32)
+    t = buf[:mt * ct * 1024].view(mt, ct, 4, 2, 32, 4)  # [mt][ct][g][h][m%32][u], c = 32ct + 8g + 4h + u
+    return t.permute(0, 4, 1, 2, 3, 5).reshape(mt * 32, ct * 32)[:M, :C]
+
+
 class _Act:
     """One activation tensor of the graph: its spatial size, channels, and the
     buffers its consumers need."""
@@ -49,7 +61,7 @@ class _Act:
     def __init__(self, H, W, C):
         self.H, self.W, self.C = H, W, C
         self.codes = {}   # consumer module -> (buffer, CodeOut)
-        self.f32 = None   # NHWC fp32 [N][H][W][C]
+        self.f32 = None   # fp32 [N*H*W][C] in the C-tile layout
 
 
 class Engine:
@@ -101,10 +113,14 @@ class Engine:
         act.codes[conv] = entry
         return entry
 
+    def _tiled(self, H, W, C):
+        t = torch.empty(ctile_numel(self.N * H * W, C), dtype=torch.float32, device=self.dev)
+        self.keep.append(t)
+        return t
+
     def _f32_for(self, act):
         if act.f32 is None:
-            act.f32 = torch.empty((self.N, act.H, act.W, act.C), dtype=torch.float32, device=self.dev)
-            self.keep.append(act.f32)
+            act.f32 = self._tiled(act.H, act.W, act.C)
         return act.f32
 
     def _bn(self, bn):
@@ -156,6 +172,7 @@ class Engine:
         if mode == 0:
             e.out_f32 = logits.data_ptr()
         else:
+            e.f32_tiled = 1  # every fp32 map of the engine (residuals, head input) is C-tile
             if bn is not None:
                 b = self._bn(bn)
                 e.bn_mean, e.bn_sq, e.bn_wq, e.bn_bq = b.mean, b.sq, b.wq, b.bq
@@ -253,25 +270,23 @@ class Engine:
             b = self._bn(bn1)
             C = conv1.out_channels
             st = _lib.stream_of(self.input)
-            dirs = torch.empty(C, dtype=torch.uint8, device=self.dev)
-            vlut = torch.empty((C, 256), dtype=torch.float32, device=self.dev)
-            _lib.call("qnn_bn_value_lut", ctypes.byref(b), C, 1, _lib.ptr(vlut), _lib.ptr(dirs), st)
             luts = []
             for co in outs:
                 lut = torch.empty((C, 256), dtype=torch.int8, device=self.dev)
                 _lib.call("qnn_bn_code_lut", ctypes.byref(b), C, 1, ctypes.byref(co), _lib.ptr(lut), st)
                 luts.append(lut)
-            self.keep += [bncode, dirs, vlut] + luts + list(outs)
+            self.keep += [bncode] + luts + list(outs)
             c0 = outs[0] if len(outs) > 0 else None
             c1 = outs[1] if len(outs) > 1 else None
             a = (N, Ho, Wo, C, pk_, ps_, pp_, Hp_, Hp_)
-            fp, qp, dp, vp = _lib.ptr(f32), _lib.ptr(bncode), _lib.ptr(dirs), _lib.ptr(vlut)
+            fp, qp = _lib.ptr(f32), _lib.ptr(bncode)
             l0 = _lib.ptr(luts[0]) if len(luts) > 0 else None
             l1 = _lib.ptr(luts[1]) if len(luts) > 1 else None
             r0 = None if c0 is None else ctypes.byref(c0)
             r1 = None if c1 is None else ctypes.byref(c1)
-            self._add("qnn_maxpool_lut", lambda st: _lib.call(
-                "qnn_maxpool_lut", qp, *a, dp, vp, fp, l0, r0, l1, r1, st))
+            br = ctypes.byref(b)
+            self._add("qnn_maxpool_bn", lambda st: _lib.call(
+                "qnn_maxpool_bn", qp, *a, br, 1, fp, 1, l0, r0, l1, r1, st))
         else:
             x_act = _Act(Ho, Wo, conv1.out_channels)
             cons, need_f32 = self._block_consumers(blocks[0])
@@ -294,8 +309,7 @@ class Engine:
         # shortcut
         if blk.downsample is not None:
             ds_conv, ds_bn = blk.downsample[0], blk.downsample[1]
-            r = torch.empty((N, Ho, Wo, cout), dtype=torch.float32, device=self.dev)
-            self.keep.append(r)
+            r = self._tiled(Ho, Wo, cout)
             self._conv(ds_conv, self._codes_for(x, ds_conv), x.H, x.W, bn=ds_bn, relu=False, out_f32=r)
             residual = r
         else:
@@ -337,13 +351,19 @@ class Engine:
                           scale=float_scale(mn, mx, fc.num_bits), qmax=_qmax(fc.num_bits))
         self.keep += [fbuf, co]
         src = x.f32
-        self.head_input = src  # NHWC fp32 feature map before the avg-pool (for tests)
+        self._head = (src, x.H, x.W, x.C)
         hw = k * k
         sp, cr, C = _lib.ptr(src), ctypes.byref(co), x.C
-        self._add("qnn_avgpool_quant", lambda st: _lib.call("qnn_avgpool_quant", sp, N, hw, C, None, cr, st))
+        self._add("qnn_avgpool_quant", lambda st: _lib.call("qnn_avgpool_quant", sp, N, hw, C, 1, None, cr, st))
         self.logits = torch.empty((N, fc.out_features), dtype=torch.float32, device=self.dev)
         geom = dict(hp=1, wp=1, cp=cp, nbytes=nbytes, range=(mn, mx))
         self._conv(fc, (fbuf, co, geom), 1, 1, mode=0, logits=self.logits)
+
+    @property
+    def head_input(self):
+        """fp32 feature map before the avg-pool as NHWC [N][H][W][C] (a copy; for tests)."""
+        src, H, W, C = self._head
+        return untile(src, self.N * H * W, C).reshape(self.N, H, W, C)
 
     # ------------------------------------------------------------------ MobileNet
     def _plan_mobilenet(self, model, hw):

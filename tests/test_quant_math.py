@@ -1,0 +1,47 @@
+"""The division-free requantizer of the HIP epilogues (qnn_internal.h quant_code_fast):
+Markstein's correction q = fma(fma(-q0, s, t), RN(1/s), q0) must equal the IEEE
+quotient RN(t/s) bit for bit, hence the same code as quantize.py:90-95.  Checked here
+on the host (gcc + libm fmaf, the same IEEE binary32 operations) on quotients packed
+around half-integers, where rint is sensitive, and on random ones."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+SRC = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+static uint64_t st = 0x9E3779B97F4A7C15ull;
+static inline uint64_t xr(void) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; }
+static inline float bits(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+int main(int argc, char** argv) {
+  long n = atol(argv[1]), bad = 0;
+  for (long it = 0; it < n; ++it) {
+    float s = bits((uint32_t)((xr() & 0x7fffff) | ((uint32_t)(100 + (int)(xr() % 36)) << 23)));
+    float inv = 1.0f / s, t;
+    if ((it & 3) == 0) {
+      t = ((float)(xr() >> 40) / 16777216.0f * 600.f - 300.f) * s;
+    } else {
+      float h = (float)((int)(xr() % 300) - 20) + 0.5f, tt = h * s;
+      uint32_t tu; memcpy(&tu, &tt, 4); tu += (int)(xr() % 9) - 4; memcpy(&t, &tu, 4);
+    }
+    float ref = t / s, q0 = t * inv, q1 = fmaf(fmaf(-q0, s, t), inv, q0);
+    if (memcmp(&q1, &ref, 4)) ++bad;
+  }
+  printf("%ld\n", bad);
+  return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_markstein_quotient_is_ieee(tmp_path):
+    c = tmp_path / "mk.c"
+    c.write_text(SRC.replace("#include <string.h>", "#include <string.h>\n#include <stdlib.h>"))
+    exe = tmp_path / "mk"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
+    out = subprocess.run([str(exe), "20000000"], check=True, capture_output=True, text=True).stdout
+    assert int(out.strip()) == 0
