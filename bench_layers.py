@@ -8,6 +8,7 @@ reported as int8 TOP/s against the 5 POPS dense peak and as algorithmic GB/s.
     python bench_layers.py [--reps 20] [--only headline]
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -61,6 +62,9 @@ def run(name, cfg, reps, dev):
         _lib.set_timer(None)
         torch.cuda.synchronize()
     d = timer.durations_ms()
+    cfg, bm, bn, nb = (ctypes.c_int() for _ in range(4))
+    _lib.call("qnn_conv_plan", *(ctypes.byref(v) for v in m._last_conv), ctypes.byref(cfg), ctypes.byref(bm),
+              ctypes.byref(bn), ctypes.byref(nb))
     conv = [ms for n, ms in d if n == "qnn_qconv2d_fwd"]
     quant = [ms for n, ms in d if n != "qnn_qconv2d_fwd"]
     conv_ms = sum(conv) / len(conv)
@@ -69,6 +73,7 @@ def run(name, cfg, reps, dev):
     ops = 2 * N * cout * Ho * Ho * cin * k * k
     bytes_conv = N * H * H * ((cin + 15) // 16 * 16) + cout * k * k * cin + 4 * N * cout * Ho * Ho
     return {"layer": name, "gemm_MxNxK": [N * Ho * Ho, cout, cin * k * k], "gop": round(ops / 1e9, 2),
+            "cfg": cfg.value, "tile": [bm.value, bn.value], "blocks": nb.value,
             "conv_us": round(conv_ms * 1e3, 2), "conv_tops": round(ops / conv_ms / 1e9, 1),
             "conv_frac": round(ops / conv_ms / 1e9 / PEAK, 4), "conv_alg_GBs": round(bytes_conv / conv_ms / 1e6, 1),
             "quantize_us": round(sum(quant) / len(quant) * 1e3, 2), "module_us": round(mod_ms * 1e3, 2)}

@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 3
+#define QNN_ABI_VERSION 5
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -125,6 +125,9 @@ typedef struct qnn_conv_desc {
                           real (tap, channel); sum_valid(q'_x) then counts only those bytes.
                           Needed by space-to-depth stems (their 2x2-tap grid over-covers the
                           kernel); NULL = every byte counts (codes past K are 0).  kpad <= 1024 */
+  int tile;            /* tile configuration: 0 = chosen by the library's cost model, k + 1 =
+                          configuration k of qnn_conv_plan (callers that autotune pass their
+                          measured best; the result is identical for every configuration) */
 } qnn_conv_desc;
 
 /* Epilogue of the contraction.  Always:
@@ -183,6 +186,11 @@ typedef struct qnn_epilogue {
  * epilogue as described by `epi`.  groups == 1 (depthwise: qnn_dwconv2d_fwd). */
 int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
                     qnn_stream_t stream);
+
+/* Tile plan qnn_qconv2d_fwd would use for this layer (introspection for benchmarks and
+ * profiles; no GPU work): configuration id, block tile (cout x pixels), grid size.
+ * QNN_CONV_CFG=<id> in the environment forces a configuration. Any out pointer may be NULL. */
+int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn, int* nblk);
 
 /* Depthwise (groups == cin == cout) eval forward: fake-quantize-on-load of x
  * (QuantMeasure range) times the dequantized weights w_hat [c][kh*kw] plus the

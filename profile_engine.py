@@ -6,6 +6,7 @@ algorithmic GB/s (codes in + weights + codes/fp32 out).
     python profile_engine.py [--depth 18] [--batch 128] [--reps 5]
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -33,6 +34,7 @@ def main():
     eng = Engine(model, batch=a.batch, graph=False)
     eng.input.copy_(synthetic.input_batch((a.batch, 3, 224, 224), 1234).to(dev))
     descs = [k for k in eng.keep if isinstance(k, _lib.ConvDesc)]
+    epis = [k for k in eng.keep if isinstance(k, _lib.Epilogue)]
     timer = _lib.LaunchTimer(set(eng.launch_names))
     with torch.no_grad():
         eng()
@@ -50,11 +52,14 @@ def main():
         row = {"i": i, "kernel": name, "us": round(ms * 1e3, 2)}
         if name == "qnn_qconv2d_fwd":
             c = descs[ci]
+            cfg, bm, bn, nb = (ctypes.c_int() for _ in range(4))
+            _lib.call("qnn_conv_plan", ctypes.byref(c), ctypes.byref(epis[ci]), ctypes.byref(cfg), ctypes.byref(bm),
+                      ctypes.byref(bn), ctypes.byref(nb))
             ci += 1
             M = c.n * c.ho * c.wo
             K = c.kh * c.kw * c.cp
             ops = 2 * M * c.cout * K
-            row.update(MxNxK=[M, c.cout, K], tops=round(ops / ms / 1e9, 1), frac=round(ops / ms / 1e9 / 5000, 4))
+            row.update(MxNxK=[M, c.cout, K], cfg=cfg.value, tile=[bm.value, bn.value], blocks=nb.value, tops=round(ops / ms / 1e9, 1), frac=round(ops / ms / 1e9 / 5000, 4))
         rows.append(row)
         print(json.dumps(row), flush=True)
     tot = sum(r["us"] for r in rows)

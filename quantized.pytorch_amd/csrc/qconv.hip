@@ -19,16 +19,17 @@
 // fp32 op order) -> + residual -> ReLU -> fp32 (C-tile or NHWC) and/or requantized
 // NHWC8 codes for up to two consumer convs (their QuantMeasure ranges).
 //
-// Block: 256 threads = 4 waves, each wave a 64x64 tile (2x2 MFMA 32x32x32).
-// K stage = BK (64 or 128) bytes; two LDS stages filled by LDS-DMA (counted vmcnt,
-// raw s_barrier), rows XOR-swizzled so ds_read_b128 fragment reads are
-// conflict-free; the stage loop is unrolled by two so every LDS address is a
-// per-lane constant plus an immediate, and fragments of k-step s+1 are read while
-// the MFMAs of step s run.  Gather addresses: the tap of each 16-byte chunk is
-// uniform per stage (or one of two) whenever Cp >= 8*BK/128, so its offset is
-// scalar arithmetic; only narrow-channel inputs use a per-lane LDS tap table.
-// Code stores: two v_permlane32_swap levels turn each lane's 4 dwords (channels
-// 8g+4h..) into 16 contiguous channels -> one 16-byte store per 32-channel group.
+// Kernel v5 (tile configurations below): 4- or 8-wave blocks, each wave a
+// (32*TM) x (32*TN) tile of 32x32x32 MFMAs.  The main loop is bound by how many
+// bytes the CU can pull from L2 into LDS per MFMA (measured ~40 B/clk/CU with
+// LDS-DMA), so blocks are as large as LDS allows: 256x256 moves 1 byte per 256
+// int8 ops (v4's 128x128: 1 per 128).  K advances in 64-byte stages through a
+// 4-slot LDS ring filled by global_load_lds_dwordx4 three stages ahead, with
+// ONE s_barrier per stage (the slot a wave refills was consumed two barriers
+// ago).  LDS rows are XOR-swizzled on the DMA source side so ds_read_b128
+// fragment reads are conflict-free.  Epilogue: per-channel parameters, border
+// table and code LUT staged in LDS; drop-in NCHW fp32 goes through a per-wave
+// LDS transpose so every global store is 16 bytes of 4 consecutive pixels.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -50,7 +51,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #endif
 #if QNN_STAMP
 // [block][wave][10]: realtime start/end, cycles in prologue / issue / wait+barrier /
-// compute / trailing barrier / epilogue, HW_ID, stages
+// compute / 0 / epilogue, HW_ID, stages
 __device__ unsigned long long qnn_dbg_stamps[1 << 20];
 __device__ unsigned long long qnn_dbg_epi[1 << 18];  // [block][wave][4]: staging, pixel state, body
 #define QNN_TSV(v)                                                                        \
@@ -74,6 +75,7 @@ constexpr int MAX_TAPS = 64;
 constexpr int MAX_CLASSES = 32;
 constexpr int MAX_MASK = 1024;
 constexpr int KPAD_ALIGN = 128;  // packed weight rows are multiples of 128 bytes (any BK divides)
+constexpr int NUM_CU = 256;
 
 enum { TAP_ONE = 0, TAP_TWO = 1, TAP_LDS = 2 };
 
@@ -85,6 +87,29 @@ struct Params {
   int lgcpt;     // log2(cp/16): 16-byte chunks per tap
   int kw_magic;  // ceil(2^16 / kw): t / kw == (t * kw_magic) >> 16 for t < 64
   int ct;        // C-tile columns, ceil(cout / 32)
+  int stagger;   // 8-wave blocks: waves 4-7 refill after computing (QNN_CONV_STAGGER=0 disables)
+  int epi_off;   // LDS byte offset of the epilogue data (stage_epi)
+  int epi_early; // 1: staged by LDS-DMA at kernel start (lands during the main loop), 0: after it
+  int scr_off;   // LDS byte offset of the NCHW transpose scratch (used after the main loop)
+};
+
+// Tile configuration: WGM x WGN waves, each (32*TM) x (32*TN) (cout x pixels), K stage
+// BK bytes, NS-slot LDS ring.
+template <int WGM_, int WGN_, int TM_, int TN_, int BK_, int NS_, int BPC_ = (WGM_ * WGN_ == 4 ? 2 : 1)>
+struct Cfg {
+  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, BK = BK_, NS = NS_;
+  static constexpr int W = WGM * WGN, NT = 64 * W;
+  static constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32;
+  static constexpr int CPR = BK / 16;    // 16-B chunks per LDS row
+  static constexpr int RPI = 1024 / BK;  // rows per 1 KiB LDS-DMA wave-instruction
+  static constexpr int NA = BM / RPI / W, NB = BN / RPI / W;  // DMA per wave per stage
+  static constexpr int STAGE = (BM + BN) * BK;
+  static constexpr int KS = BK / 32;  // MFMA k-steps per stage
+  static constexpr int P = NA + NB;
+  static constexpr int BPC = BPC_;  // resident blocks per CU the LDS budget must allow
+  static_assert((BM / RPI) % W == 0 && (BN / RPI) % W == 0, "DMA rows must split evenly over the waves");
+  static_assert(BK == 64 || BK == 128, "BK");
+  static_assert(NS >= 3 && NS <= 4, "ring depth");
 };
 
 // Byte offset of 16-byte chunk `chunk` of LDS row `row` (rows of BK bytes): XOR swizzle so
@@ -148,15 +173,91 @@ static inline int epi_kind(const qnn_epilogue& e) {
   return EK_GEN;
 }
 
-// Epilogue LDS bytes: params [7][BM] fp32, border table [nclass][BM] fp32, LUT [BM][256].
-static inline int epi_lds_bytes(const qnn_epilogue& e, int BM) {
-  return 4 * (7 + e.nclass) * BM + (epi_kind(e) == EK_LUT ? 256 * BM : 0);
+
+// y for channels cl..cl+3 (register group g of an accumulator): the exact decomposition
+// s_x*s_w*acc + s_x*b_w*sum_valid(q'_x) + border term, + bias; parameters read as float4.
+__device__ __forceinline__ void conv_out4(const float* s_f, int BM, int cl, int ptab, float psq, const v16i& a, int g,
+                                          float (&v)[4]) {
+  const float4 sw = *reinterpret_cast<const float4*>(s_f + cl);
+  const float4 bw = *reinterpret_cast<const float4*>(s_f + BM + cl);
+  const float4 tb = *reinterpret_cast<const float4*>(s_f + ptab + cl);
+  const float4 bi = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
+  v[0] = fmaf(sw.x, (float)a[4 * g + 0], fmaf(bw.x, psq, tb.x)) + bi.x;
+  v[1] = fmaf(sw.y, (float)a[4 * g + 1], fmaf(bw.y, psq, tb.y)) + bi.y;
+  v[2] = fmaf(sw.z, (float)a[4 * g + 2], fmaf(bw.z, psq, tb.z)) + bi.z;
+  v[3] = fmaf(sw.w, (float)a[4 * g + 3], fmaf(bw.w, psq, tb.w)) + bi.w;
+}
+
+// Epilogue data in LDS at p.epi_off (f32 unless noted):
+//   [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq
+//   [7BM, (7+nclass)BM) border table [cls][BM]  then (EK_LUT) int8 LUT [BM][256]
+// moved by LDS-DMA (4 bytes per lane for the vectors and the table, 16 for the LUT), one
+// job per wave-instruction, so the whole staging is ~8 DMA per wave and one round trip.
+// Channels past cout read channel cout-1 (their outputs are never stored).
+template <class C, int EK>
+__device__ __forceinline__ void stage_epi(const Params& p, const int8_t* x, int8_t* dst, int c0, int wave, int lane) {
+  constexpr int BM = C::BM, W = C::W, CH = BM / 64;  // 64-float chunks per vector
+  const qnn_epilogue& e = p.e;
+  const int cmax = p.d.cout - 1;
+  const int nvec = (EK != EK_NCHW && e.bn_mean) ? 7 : 3;
+  const int nf = (nvec + e.nclass) * CH;
+  for (int jb = wave; jb < nf; jb += W) {
+    const int v = jb / CH, k = jb - v * CH;
+    const int arr = v < nvec ? v : 7 + (v - nvec);
+    int c = c0 + 64 * k + lane;
+    c = c < cmax ? c : cmax;
+    const float* src;
+    switch (arr) {
+      case 0: src = e.sxsw; break;
+      case 1: src = e.sxbw; break;
+      case 2:  // no bias: zeros from the input's 128-byte zero page
+        if (!e.bias) {
+          src = reinterpret_cast<const float*>(x + p.d.zero_off);
+          c = lane & 31;
+        } else {
+          src = e.bias;
+        }
+        break;
+      case 3: src = e.bn_mean; break;
+      case 4: src = e.bn_sq; break;
+      case 5: src = e.bn_wq; break;
+      case 6: src = e.bn_bq; break;
+      default: src = e.table + (int64_t)(arr - 7) * p.d.cout; break;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)(src + c), (lds_ptr_t)(dst + 4 * (arr * BM + 64 * k)), 4, 0, 0);
+  }
+  if constexpr (EK == EK_LUT) {
+    int8_t* lut = dst + 4 * (7 + e.nclass) * BM;
+    for (int jl = wave; jl < BM / 4; jl += W) {
+      int c = c0 + 4 * jl + (lane >> 4);
+      c = c < cmax ? c : cmax;
+      __builtin_amdgcn_global_load_lds((const void*)(e.lut + (int64_t)c * 256 + 16 * (lane & 15)),
+                                       (lds_ptr_t)(lut + 1024 * jl), 16, 0, 0);
+    }
+  }
+}
+
+// Border-table class of each of this lane's TN pixels (computed before the main loop so
+// the hcls / wcls loads complete under it).
+template <class C>
+__device__ __forceinline__ void pixel_classes(const Params& p, int m0, int wn, int lane, int (&pcls)[C::TN]) {
+  const int HoWo = p.d.ho * p.d.wo;
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j) {
+    int m = m0 + wn * 32 * C::TN + j * 32 + (lane & 31);
+    m = m < p.M ? m : p.M - 1;
+    const int n = m / HoWo, hw = m - n * HoWo, ho = hw / p.d.wo, wo = hw - ho * p.d.wo;
+    pcls[j] = p.e.hcls[ho] * p.e.nwc + p.e.wcls[wo];
+  }
 }
 
 // sumq[j]: full receptive-field sum of q'_x for this lane's pixel of column tile j.
-template <int BM, int EK>
-__device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], const int (&sumq)[2], int8_t* smem,
-                                         int m0, int c0, int wm, int wn, int lane, int tid) {
+// The epilogue data is staged (stage_epi) and visible (barrier) on entry.
+template <class C, int EK>
+__device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::TN], const int (&sumq)[C::TN],
+                                         const int (&pcls)[C::TN], int8_t* smem, int m0, int c0, int wm, int wn,
+                                         int lane, int tid, int wave) {
+  constexpr int BM = C::BM, TM = C::TM, TN = C::TN;
   const qnn_conv_desc& d = p.d;
   const qnn_epilogue& e = p.e;
   const int frow = lane & 31, fh = lane >> 5;
@@ -165,96 +266,72 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
   unsigned long long e0 = 0, e1 = 0, e2 = 0, e3 = 0;
 #endif
   QNN_TSV(e0);
-
-  // residual prefetch, 8 float4 (one 32-channel half) at a time: half 0 before the
-  // parameter staging, half 1 while half 0 is processed (each load would otherwise be
-  // a serialized HBM round trip)
-  float4 res[2][2][4];
-  const bool has_res = EK == EK_GEN && e.residual != nullptr;
-  auto load_res = [&](int i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      int m = m0 + wn * 64 + j * 32 + frow;
-      if (m > p.M - 1) m = p.M - 1;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        int c = c0 + wm * 64 + i * 32 + 8 * g + 4 * fh;
-        if (c > d.cout - 4) c = d.cout - 4;
-        const int64_t fi = e.f32_tiled ? ctile_index(m, c, p.ct) : (int64_t)m * d.cout + c;
-        res[i][j][g] = *reinterpret_cast<const float4*>(e.residual + fi);
-      }
-    }
-  };
-  if (EK == EK_GEN && has_res) load_res(0);
-
-  float* s_f = reinterpret_cast<float*>(smem);  // main-loop LDS is free now
-  // [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq  [7BM..) table[cls][BM]
+  const float* s_f = reinterpret_cast<const float*>(smem + p.epi_off);
   const int nparam = 7 * BM;
-  for (int i = tid; i < BM; i += 256) {
-    const int c = c0 + i;
-    const bool ok = c < d.cout;
-    s_f[i] = ok ? e.sxsw[c] : 0.f;
-    s_f[BM + i] = ok ? e.sxbw[c] : 0.f;
-    s_f[2 * BM + i] = (ok && e.bias) ? e.bias[c] : 0.f;
-    if (EK != EK_NCHW && e.bn_mean) {
-      s_f[3 * BM + i] = ok ? e.bn_mean[c] : 0.f;
-      s_f[4 * BM + i] = ok ? e.bn_sq[c] : 0.f;
-      s_f[5 * BM + i] = ok ? e.bn_wq[c] : 0.f;
-      s_f[6 * BM + i] = ok ? e.bn_bq[c] : 0.f;
-    }
-  }
-  for (int i = tid; i < e.nclass * BM; i += 256) {
-    const int cls = i / BM, c = c0 + (i - cls * BM);
-    s_f[nparam + i] = c < d.cout ? e.table[cls * d.cout + c] : 0.f;
-  }
-  int8_t* s_lut = smem + 4 * (7 + e.nclass) * BM;  // [BM][256] next-layer codes (EK_LUT)
-  if constexpr (EK == EK_LUT) {
-#pragma unroll
-    for (int k = 0; k < BM * 16 / 256; ++k) {
-      const int i = tid + 256 * k;
-      const int c = c0 + (i >> 4);
-      v4i v = {0, 0, 0, 0};
-      if (c < d.cout) v = *reinterpret_cast<const v4i*>(e.lut + (int64_t)c * 256 + 16 * (i & 15));
-      *reinterpret_cast<v4i*>(s_lut + 16 * i) = v;
-    }
-  }
-  __syncthreads();
+  const int8_t* s_tail = smem + p.epi_off + 4 * (7 + e.nclass) * BM;  // LUT [BM][256] (EK_LUT)
   QNN_TSV(e1);
 
-  // per-pixel (lane) state for the two 32-pixel column tiles of this wave
-  int pm[2], pn[2], phw[2], pho[2], pwo[2], ptab[2];
-  float psq[2];
+  // per-pixel (lane) state for the TN 32-pixel column tiles of this wave
+  int pm[TN], pn[TN], pho[TN], pwo[TN], ptab[TN];
+  float psq[TN];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int m = m0 + wn * 64 + j * 32 + frow;
+  for (int j = 0; j < TN; ++j) {
+    const int m = m0 + wn * 32 * TN + j * 32 + frow;
     pm[j] = m;
     const int mm = m < p.M ? m : p.M - 1;
     pn[j] = mm / HoWo;
-    phw[j] = mm - pn[j] * HoWo;
-    pho[j] = phw[j] / d.wo;
-    pwo[j] = phw[j] - pho[j] * d.wo;
-    ptab[j] = nparam + (e.hcls[pho[j]] * e.nwc + e.wcls[pwo[j]]) * BM;
+    const int hw = mm - pn[j] * HoWo;
+    pho[j] = hw / d.wo;
+    pwo[j] = hw - pho[j] * d.wo;
+    ptab[j] = nparam + pcls[j] * BM;
     psq[j] = (float)sumq[j];
   }
   QNN_TSV(e2);
 
   if constexpr (EK == EK_NCHW) {
-    // drop-in output: NCHW fp32 (lanes = consecutive pixels of one channel plane)
+    // drop-in output: NCHW fp32.  Each 32x32 sub-tile goes through this wave's LDS
+    // scratch ([32 channels][32 pixels], conflict-free both ways) so that a lane then
+    // holds 4 consecutive pixels of one channel: one 16-byte store (needs HoWo % 4 == 0,
+    // so 4 consecutive pixels never straddle images; else one scalar store per value).
+    float* scr = reinterpret_cast<float*>(smem + p.scr_off) + wave * 1024;
+    const bool vec = (HoWo & 3) == 0;
+    const int q4 = lane & 7, rsub = lane >> 3;  // read phase: pixel quad, row within 8
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int j = 0; j < TN; ++j) {
+      const int mq = m0 + wn * 32 * TN + j * 32 + 4 * q4;  // first pixel of this lane's quad
+      const int mqc = mq < p.M ? mq : p.M - 1;
+      const int nq = mqc / HoWo, hwq = mqc - nq * HoWo;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;
-        const int c = c0 + cl;
+      for (int i = 0; i < TM; ++i) {
+        const int clb = wm * 32 * TM + i * 32;  // local channel base of this sub-tile
+        float y[16];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (pm[j] >= p.M) continue;
-          float* yp = e.out_f32 + ((int64_t)pn[j] * d.cout + c) * HoWo + phw[j];
+        for (int g = 0; g < 4; ++g) {
+          const int cl = clb + 8 * g + 4 * fh;
+          float yg[4];
+          conv_out4(s_f, BM, cl, ptab[j], psq[j], acc[i][j], g, yg);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float y = fmaf(s_f[cl + u], (float)acc[i][j][4 * g + u],
-                                 fmaf(s_f[BM + cl + u], psq[j], s_f[ptab[j] + cl + u]));
-            if (c + u < d.cout) yp[(int64_t)u * HoWo] = y + s_f[2 * BM + cl + u];
+          for (int u = 0; u < 4; ++u) y[4 * g + u] = yg[u];
+        }
+        if (vec) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) scr[(8 * (r >> 2) + 4 * fh + (r & 3)) * 32 + frow] = y[r];
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int row = 8 * k + rsub;
+            const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + 4 * q4);
+            const int c = c0 + clb + row;
+            if (mq < p.M && c < d.cout)
+              *reinterpret_cast<float4*>(e.out_f32 + ((int64_t)nq * d.cout + c) * HoWo + hwq) = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+        } else if (pm[j] < p.M) {
+          float* yp = e.out_f32 + (int64_t)pn[j] * d.cout * HoWo + (pm[j] - pn[j] * HoWo);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = c0 + clb + 8 * (r >> 2) + 4 * fh + (r & 3);
+            if (c < d.cout) yp[(int64_t)c * HoWo] = y[r];
           }
         }
       }
@@ -264,33 +341,45 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
     const CodeDst t0 = {e.out_code0, e.code0_cp, e.code0_pad, e.code0_hp, e.code0_wp};
     const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
     const CodeDst tb = {reinterpret_cast<int8_t*>(e.out_bncode), d.cout, 0, d.ho, d.wo};
+    const bool has_res = EK == EK_GEN && e.residual != nullptr;
+    // residual of sub-tile (i, j): 4 float4 per lane, fetched one sub-tile ahead
+    auto load_res = [&](float4 (&r)[4], int i, int j) {
+      const int m = pm[j] < p.M ? pm[j] : p.M - 1;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (EK == EK_GEN && has_res && i == 0) load_res(1);
-      const int cb = c0 + wm * 64 + i * 32;  // first channel of this lane's 32-channel group
+      for (int g = 0; g < 4; ++g) {
+        int c = c0 + wm * 32 * TM + i * 32 + 8 * g + 4 * fh;
+        if (c > d.cout - 4) c = d.cout - 4;
+        const int64_t fi = e.f32_tiled ? ctile_index(m, c, p.ct) : (int64_t)m * d.cout + c;
+        r[g] = *reinterpret_cast<const float4*>(e.residual + fi);
+      }
+    };
+    float4 rcur[4], rnxt[4];
+    if (EK == EK_GEN && has_res) load_res(rcur, 0, 0);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+    for (int i = 0; i < TM; ++i) {
+      const int cb = c0 + wm * 32 * TM + i * 32;  // first channel of this lane's 32-channel group
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (EK == EK_GEN && has_res) {
+          if (j + 1 < TN) load_res(rnxt, i, j + 1);
+          else if (i + 1 < TM) load_res(rnxt, i + 1, 0);
+        }
         const bool pok = pm[j] < p.M;
         int k0[4], k1[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int cl = wm * 64 + i * 32 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
+          const int cl = cb - c0 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
           const int c = c0 + cl;
           const bool cok = c < d.cout;  // cout % 16 == 0: a 4-channel group is all in or all out
           float v[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float y = fmaf(s_f[cl + u], (float)acc[i][j][4 * g + u],
-                                 fmaf(s_f[BM + cl + u], psq[j], s_f[ptab[j] + cl + u]));
-            v[u] = y + s_f[2 * BM + cl + u];
-          }
+          conv_out4(s_f, BM, cl, ptab[j], psq[j], acc[i][j], g, v);
           k0[g] = k1[g] = 0;
           if constexpr (EK == EK_LUT) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated (exact)
             int r = 0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
-              r |= ((int)(uint8_t)s_lut[(cl + u) * 256 + q]) << (8 * u);
+              r |= ((int)(uint8_t)s_tail[(cl + u) * 256 + q]) << (8 * u);
             }
             k0[g] = cok ? r : 0;
             continue;
@@ -306,18 +395,23 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
             continue;
           } else {
             if (e.bn_mean) {
+              const float4 mn4 = *reinterpret_cast<const float4*>(s_f + 3 * BM + cl);
+              const float4 sq4 = *reinterpret_cast<const float4*>(s_f + 4 * BM + cl);
+              const float4 wq4 = *reinterpret_cast<const float4*>(s_f + 5 * BM + cl);
+              const float4 bq4 = *reinterpret_cast<const float4*>(s_f + 6 * BM + cl);
+              const float mn[4] = {mn4.x, mn4.y, mn4.z, mn4.w}, sq[4] = {sq4.x, sq4.y, sq4.z, sq4.w};
+              const float wq[4] = {wq4.x, wq4.y, wq4.z, wq4.w}, bq[4] = {bq4.x, bq4.y, bq4.z, bq4.w};
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
-                const int l = cl + u;
-                float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - s_f[3 * BM + l];  // x - mean
-                o = o * s_f[4 * BM + l];                                                   // * q(scale)
-                o = o * s_f[5 * BM + l];                                                   // * q(weight)
-                v[u] = o + s_f[6 * BM + l];                                                // + q(bias)
+                float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - mn[u];  // x - mean
+                o = o * sq[u];                                                   // * q(scale)
+                o = o * wq[u];                                                   // * q(weight)
+                v[u] = o + bq[u];                                                // + q(bias)
               }
             }
             float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
             if (has_res) {
-              const float4 r4 = res[i][j][g];
+              const float4 r4 = rcur[g];
               o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
             }
             if (e.relu) {
@@ -348,40 +442,37 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[2][2], con
           if (EK == EK_GEN && e.out_code1)
             store_codes(t1, pn[j], pho[j], pwo[j], ch, pok, gather16(k1[0], k1[1], k1[2], k1[3]));
         }
+        if (EK == EK_GEN && has_res) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) rcur[g] = rnxt[g];
+        }
       }
     }
   }
 #if QNN_STAMP
   QNN_TSV(e3);
-  if (lane == 0 && blockIdx.x < (1 << 18) / 16) {
-    unsigned long long* o = qnn_dbg_epi + ((size_t)blockIdx.x * 4 + (tid >> 6)) * 4;
+  if (lane == 0 && blockIdx.x < (1 << 18) / (4 * C::W)) {
+    unsigned long long* o = qnn_dbg_epi + ((size_t)blockIdx.x * C::W + wave) * 4;
     o[0] = e1 - e0; o[1] = e2 - e1; o[2] = e3 - e2; o[3] = 0;
   }
 #endif
 }
 
-template <int BM, int BN, int BK, int EK, int TAPM, bool MASKED>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GEN ? 2 : 3))) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
-                                                    const Params p) {
-  constexpr int WM = BM / 64, WN = BN / 64;
-  static_assert(WM * WN == 4, "4 waves of 64x64");
-  static_assert(BK == 64 || BK == 128, "BK");
+template <class C, int EK, int TAPM, bool MASKED>
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+                                                      const Params p) {
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NS = C::NS, W = C::W, TM = C::TM, TN = C::TN;
+  constexpr int CPR = C::CPR, RPI = C::RPI, NA = C::NA, NB = C::NB, STAGE = C::STAGE, KS = C::KS, P = C::P;
   static_assert(!MASKED || TAPM == TAP_LDS, "masked (space-to-depth) stems use the LDS tap table");
-  constexpr int CPR = BK / 16;        // 16-B chunks per LDS row
-  constexpr int RPI = 1024 / BK;      // rows per 1 KiB LDS-DMA wave-instruction
-  constexpr int NA = BM / (4 * RPI);  // glds per wave per stage for A
-  constexpr int NB = BN / (4 * RPI);
-  constexpr int STAGE = (BM + BN) * BK;
-  constexpr int KS = BK / 32;  // MFMA k-steps per stage
   // one dynamic LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  int* s_tap = reinterpret_cast<int*>(smem + 2 * STAGE);
-  int8_t* s_mask = smem + 2 * STAGE + 4 * MAX_TAPS;
+  int* s_tap = reinterpret_cast<int*>(smem + NS * STAGE);
+  int8_t* s_mask = smem + NS * STAGE + 4 * MAX_TAPS;
 
   const qnn_conv_desc& d = p.d;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
 
   // ---- XCD-aware, bijective block -> tile map: each XCD gets a contiguous run of
   // tiles, output-channel tiles fastest so blocks sharing an activation tile share L2
@@ -401,18 +492,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
     if (tid < p.taps) s_tap[tid] = ((tid / d.kw) * d.wp + (tid % d.kw)) * d.cp;
   }
   if constexpr (MASKED) {
-    for (int i = tid; i < d.kpad / 16; i += 256)
+    for (int i = tid; i < d.kpad / 16; i += C::NT)
       *reinterpret_cast<v4i*>(s_mask + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
   }
 
   // ---- per-lane gather state: B chunk (row, slot) -> pixel base + chunk-in-tap offset,
-  // and which of the stage's taps the chunk belongs to
+  // and which of the stage's taps the chunk belongs to.  DMA instruction i of the B
+  // (A) image covers rows [i*RPI, (i+1)*RPI); wave w issues i = w, w + W, ...
   const int cpt_mask = (1 << p.lgcpt) - 1;
   uint32_t bbase[NB];
   int bdelta[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int row = RPI * (wave + 4 * j) + lane / CPR;
+    const int row = RPI * (wave + W * j) + lane / CPR;
     int m = m0 + row;
     if (m > p.M - 1) m = p.M - 1;
     const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
@@ -424,22 +516,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
   uint32_t aoff[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int row = RPI * (wave + 4 * j) + lane / CPR;
-    aoff[j] = (uint32_t)(row * d.kpad + (swz<BK>(row, lane % CPR) - row * BK));
+    const int row = RPI * (wave + W * j) + lane / CPR;
+    const int crow = (c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0);  // never past the packed rows
+    aoff[j] = (uint32_t)(crow * d.kpad + (swz<BK>(row, lane % CPR) - row * BK));
   }
+  int pcls[TN];
+  pixel_classes<C>(p, m0, wn, lane, pcls);
+  if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
   if constexpr (TAPM == TAP_LDS || MASKED) __syncthreads();  // s_tap / s_mask
 
-  auto issue = [&](int st, int buf) {
+  auto issue = [&](int st, int slot) {
     if (QNN_ABLATE == 1) return;
-    int8_t* sa = smem + buf * STAGE;
+    int8_t* sa = smem + slot * STAGE;
     int8_t* sb = sa + BM * BK;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       uint32_t off = aoff[j] + (uint32_t)(st * BK);
       asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(sa + (wave + 4 * j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(sa + (wave + W * j) * 1024), 16, 0, 0);
     }
-    const int t0 = (st * CPR) >> p.lgcpt;                       // first tap of this stage
+    const int t0 = (st * CPR) >> p.lgcpt;                           // first tap of this stage
     const uint32_t uin = (uint32_t)(((st * CPR) & cpt_mask) << 4);  // chunk-in-tap part (cp > 16*CPR)
     const uint32_t zoff = (uint32_t)d.zero_off;
     uint32_t T0 = 0, T1 = 0;
@@ -465,16 +561,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
         off = tap < p.taps ? bbase[j] + uin + to : zoff;
       }
       asm volatile("" : "+v"(off));  // keep ONE per-lane-address load (no saddr/vaddr branch split)
-      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wave + 4 * j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wave + W * j) * 1024), 16, 0, 0);
     }
   };
 
-  v16i acc[2][2];
+  v16i acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (v16i){0};
-  int sumq[2] = {0, 0};
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v16i){0};
+  int sumq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) sumq[j] = 0;
 
   // per-lane fragment offsets of each k-step (the XOR swizzle depends only on frow)
   const int frow = lane & 31, fh = lane >> 5;
@@ -482,18 +580,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int xo = swz<BK>(frow, 2 * ks + fh) - frow * BK;
-    offa[ks] = (wm * 64 + frow) * BK + xo;
-    offb[ks] = BM * BK + (wn * 64 + frow) * BK + xo;
+    offa[ks] = (wm * 32 * TM + frow) * BK + xo;
+    offb[ks] = BM * BK + (wn * 32 * TN + frow) * BK + xo;
   }
 
-  auto compute = [&](auto bufc, int st) {
-    constexpr int BO = decltype(bufc)::value * STAGE;
-    v4i fa[2][2], fb[2][2];
-    auto load = [&](int ks, int slot) {
+  auto compute = [&](auto slotc, int st) {
+    constexpr int BO = decltype(slotc)::value * STAGE;
+    v4i fa[2][TM], fb[2][TN];
+    auto load = [&](int ks, int sl) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[slot][i] = *reinterpret_cast<const v4i*>(smem + BO + offa[ks] + i * 32 * BK);
+      for (int i = 0; i < TM; ++i) fa[sl][i] = *reinterpret_cast<const v4i*>(smem + BO + offa[ks] + i * 32 * BK);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[slot][j] = *reinterpret_cast<const v4i*>(smem + BO + offb[ks] + j * 32 * BK);
+      for (int j = 0; j < TN; ++j) fb[sl][j] = *reinterpret_cast<const v4i*>(smem + BO + offb[ks] + j * 32 * BK);
     };
     load(0, 0);
 #pragma unroll
@@ -503,16 +601,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
       v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
       if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(s_mask + st * BK + 16 * (2 * ks + fh));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < TN; ++j) {
         int s = __builtin_amdgcn_sdot4(fb[cur][j].x, ones.x, sumq[j], false);
         s = __builtin_amdgcn_sdot4(fb[cur][j].y, ones.y, s, false);
         s = __builtin_amdgcn_sdot4(fb[cur][j].z, ones.z, s, false);
         sumq[j] = __builtin_amdgcn_sdot4(fb[cur][j].w, ones.w, s, false);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < TN; ++j) {
           if (QNN_ABLATE == 2) {
             asm volatile("" ::"v"(fa[cur][i]), "v"(fb[cur][j]));
             acc[i][j][0] += fa[cur][i].x;
@@ -524,56 +622,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
   };
 
   const int nstage = d.kpad / BK;
+  const bool late = p.stagger && wave >= 4;
 #if QNN_STAMP
-  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, c_iss = 0, c_wait = 0, c_comp = 0, c_bar = 0;
+  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, c_iss = 0, c_wait = 0, c_comp = 0;
   const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
   __builtin_amdgcn_s_waitcnt(0xC07F);
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
-  issue(0, 0);
-  auto step = [&](auto bufc, int st) {
-    constexpr int b = decltype(bufc)::value;
+  // prologue: NS-1 stages in flight
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nstage) issue(s, s);
+
+  // stage st lives in slot st % NS.  Before the barrier of step st every wave waits for
+  // its own DMA of stage st (the younger stages st+1 .. st+NS-2 may stay in flight);
+  // after it, all of stage st is in LDS and every wave has finished stage st-1, whose
+  // slot (st+NS-1) % NS is refilled with stage st+NS-1.
+  auto step = [&](auto slotc, int st) {
+    constexpr int SL = decltype(slotc)::value;
     QNN_TS(ts0);
-    if (st + 1 < nstage) {
-      issue(st + 1, b ^ 1);
-      QNN_TS(ts1);
-      wait_vmcnt<NA + NB>();
-    } else {
-      QNN_TS(ts1);
-      wait_vmcnt<0>();
-    }
+    const int ahead = nstage - 1 - st;  // stages issued after st (capped at NS-2)
+    if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * P>();
+    else if (NS == 4 && ahead == 1) wait_vmcnt<P>();
+    else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
+    QNN_TS(ts1);
+    // stagger: the two waves sharing a SIMD (w, w + 4) split roles within the stage — the
+    // low half issues its DMA first while the high half's MFMAs keep the matrix pipe busy,
+    // then the high half issues while the low half computes
+    const bool refill = st + NS - 1 < nstage;
+    if (!late && refill) issue(st + NS - 1, (SL + NS - 1) % NS);
     QNN_TS(ts2);
-    compute(bufc, st);
+    compute(slotc, st);
+    if (late && refill) issue(st + NS - 1, (SL + NS - 1) % NS);
     QNN_TS(ts3);
-    __builtin_amdgcn_s_barrier();
-    QNN_TS(ts4);
 #if QNN_STAMP
-    c_iss += ts1 - ts0;
-    c_wait += ts2 - ts1;
+    c_wait += ts1 - ts0;
+    c_iss += ts2 - ts1;
     c_comp += ts3 - ts2;
-    c_bar += ts4 - ts3;
 #endif
   };
 #if QNN_STAMP
   QNN_TS(ts0);
   const unsigned long long c_pro = ts0 - t_begin;
 #endif
-  for (int st = 0; st < nstage; st += 2) {
+  for (int st = 0; st < nstage; st += NS) {
     step(std::integral_constant<int, 0>{}, st);
     if (st + 1 < nstage) step(std::integral_constant<int, 1>{}, st + 1);
+    if (st + 2 < nstage) step(std::integral_constant<int, 2>{}, st + 2);
+    if constexpr (NS == 4)
+      if (st + 3 < nstage) step(std::integral_constant<int, 3>{}, st + 3);
   }
 
 #pragma unroll
-  for (int j = 0; j < 2; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
+  for (int j = 0; j < TN; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
   __syncthreads();  // main-loop LDS is reused by the epilogue
   if (QNN_ABLATE == 3) {
     int z = sumq[0];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) z ^= acc[i][j][r];
     if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;  // keeps every MFMA live, (almost) never stores
@@ -582,68 +692,428 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EK == EK_GE
 #if QNN_STAMP
   QNN_TS(ts0);
 #endif
-  epilogue<BM, EK>(p, acc, sumq, smem, m0, c0, wm, wn, lane, tid);
+  if (!p.epi_early) {  // no room beside the ring: stage into it now
+    stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+  epilogue<C, EK>(p, acc, sumq, pcls, smem, m0, c0, wm, wn, lane, tid, wave);
 #if QNN_STAMP
   QNN_TS(ts1);
   const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
   __builtin_amdgcn_s_waitcnt(0xC07F);
   unsigned hwid;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-  if (lane == 0 && blockIdx.x < (1 << 20) / 40) {
-    unsigned long long* o = qnn_dbg_stamps + ((size_t)blockIdx.x * 4 + wave) * 10;
-    o[0] = rt_start; o[1] = rt_end; o[2] = c_pro; o[3] = c_iss; o[4] = c_wait; o[5] = c_comp; o[6] = c_bar;
+  if (lane == 0 && blockIdx.x < (1 << 20) / (10 * W)) {
+    unsigned long long* o = qnn_dbg_stamps + ((size_t)blockIdx.x * W + wave) * 10;
+    o[0] = rt_start; o[1] = rt_end; o[2] = c_pro; o[3] = c_iss; o[4] = c_wait; o[5] = c_comp; o[6] = 0;
     o[7] = ts1 - ts0; o[8] = hwid; o[9] = nstage;
   }
 #endif
 }
 
-template <int BM, int BN, int BK>
-static int main_lds_bytes(int tapm, bool masked) {
-  return 2 * (BM + BN) * BK + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
+// ---------------------------------------------------------------- ping-pong main loop
+// 8-wave blocks (waves w and w + 4 share a SIMD).  The K loop runs in PHASES of KPP
+// k-steps; each phase is [load segment: ds_read this phase's fragments, issue part of
+// the LDS-DMA of K-tile t+2] s_barrier [MFMA segment: the phase's MFMAs] s_barrier.
+// Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave is in its MFMA
+// segment while its partner loads: the matrix pipe never waits for ds_read / DMA issue.
+// LDS ring of 4 K-tiles; K-tile t+2 is written into the slot of t-2, whose last ds_read
+// retired (lgkmcnt) two phases earlier.  Before the last phase's barrier of K-tile t each
+// wave waits (vmcnt) for its own DMA of K-tile t+1, which is first read a phase later.
+template <class C, int KPP, int EK, int TAPM, bool MASKED>
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(2))) void qconv_pp_kernel(
+    const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p) {
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NS = C::NS, W = C::W, TM = C::TM, TN = C::TN;
+  constexpr int CPR = C::CPR, RPI = C::RPI, NA = C::NA, NB = C::NB, STAGE = C::STAGE, KS = C::KS, P = C::P;
+  constexpr int PPT = KS / KPP;  // phases per K-tile
+  static_assert(W == 8 && NS == 4 && KS % KPP == 0, "ping-pong: 8 waves, 4-slot ring");
+  static_assert(!MASKED || TAPM == TAP_LDS, "masked (space-to-depth) stems use the LDS tap table");
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  int* s_tap = reinterpret_cast<int*>(smem + NS * STAGE);
+  int8_t* s_mask = smem + NS * STAGE + 4 * MAX_TAPS;
+
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  const bool late = wave >= 4;
+
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nbx = (p.M + BN - 1) / BN;
+  const int nblk = nbx * nby;
+  int t;
+  {
+    const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int m0 = (t / nby) * BN;
+  const int c0 = (t % nby) * BM;
+  const int HoWo = d.ho * d.wo;
+
+  if constexpr (TAPM == TAP_LDS) {
+    if (tid < p.taps) s_tap[tid] = ((tid / d.kw) * d.wp + (tid % d.kw)) * d.cp;
+  }
+  if constexpr (MASKED) {
+    for (int i = tid; i < d.kpad / 16; i += C::NT)
+      *reinterpret_cast<v4i*>(s_mask + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
+  }
+  const int cpt_mask = (1 << p.lgcpt) - 1;
+  uint32_t bbase[NB];
+  int bdelta[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int row = RPI * (wave + W * j) + lane / CPR;
+    int m = m0 + row;
+    if (m > p.M - 1) m = p.M - 1;
+    const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
+    const int bch = (swz<BK>(row, lane % CPR) - row * BK) >> 4;
+    bbase[j] = (uint32_t)(((n * d.hp + ho * d.sh) * d.wp + wo * d.sw) * d.cp) + ((bch & cpt_mask) << 4);
+    bdelta[j] = bch >> p.lgcpt;
+  }
+  const int8_t* wblk = w + (int64_t)c0 * d.kpad;
+  uint32_t aoff[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int row = RPI * (wave + W * j) + lane / CPR;
+    const int crow = (c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0);
+    aoff[j] = (uint32_t)(crow * d.kpad + (swz<BK>(row, lane % CPR) - row * BK));
+  }
+  int pcls[TN];
+  pixel_classes<C>(p, m0, wn, lane, pcls);
+  if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
+  if constexpr (TAPM == TAP_LDS || MASKED) __syncthreads();
+
+  const int nstage = d.kpad / BK;
+  // DMA of K-tile st (clamped to the last tile: the ring slots past the end are free, so
+  // re-reading valid bytes into them keeps every wave's DMA count uniform) into `slot`;
+  // part q of PPT: the A rows and B rows are split over the phases of a K-tile.
+  auto issue = [&](int st, int slot, int q) {
+    if (QNN_ABLATE == 1) return;
+    if (st > nstage - 1) st = nstage - 1;
+    int8_t* sa = smem + slot * STAGE;
+    int8_t* sb = sa + BM * BK;
+    if (PPT == 1 || q == 0) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        uint32_t off = aoff[j] + (uint32_t)(st * BK);
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(sa + (wave + W * j) * 1024), 16, 0, 0);
+      }
+    }
+    if (PPT == 1 || q == PPT - 1) {
+      const int t0 = (st * CPR) >> p.lgcpt;
+      const uint32_t uin = (uint32_t)(((st * CPR) & cpt_mask) << 4);
+      const uint32_t zoff = (uint32_t)d.zero_off;
+      uint32_t T0 = 0, T1 = 0;
+      bool v0 = false, v1 = false;
+      if constexpr (TAPM != TAP_LDS) {
+        v0 = t0 < p.taps;
+        T0 = (uint32_t)tap_offset(p, t0) + uin;
+        if constexpr (TAPM == TAP_TWO) {
+          v1 = t0 + 1 < p.taps;
+          T1 = (uint32_t)tap_offset(p, t0 + 1);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        uint32_t off;
+        if constexpr (TAPM == TAP_ONE) {
+          off = v0 ? bbase[j] + T0 : zoff;
+        } else if constexpr (TAPM == TAP_TWO) {
+          off = bdelta[j] ? (v1 ? bbase[j] + T1 : zoff) : (v0 ? bbase[j] + T0 : zoff);
+        } else {
+          const int tap = t0 + bdelta[j];
+          const uint32_t to = (uint32_t)s_tap[tap < MAX_TAPS ? tap : MAX_TAPS - 1];
+          off = tap < p.taps ? bbase[j] + uin + to : zoff;
+        }
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wave + W * j) * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  v16i acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v16i){0};
+  int sumq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) sumq[j] = 0;
+
+  const int frow = lane & 31, fh = lane >> 5;
+  int offa[KS], offb[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int xo = swz<BK>(frow, 2 * ks + fh) - frow * BK;
+    offa[ks] = (wm * 32 * TM + frow) * BK + xo;
+    offb[ks] = BM * BK + (wn * 32 * TN + frow) * BK + xo;
+  }
+
+  v4i fa[KPP][TM], fb[KPP][TN];
+  auto read_frags = [&](auto slotc, int q) {
+    constexpr int BO = decltype(slotc)::value * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < KPP; ++kk) {
+      const int ks = q * KPP + kk;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[kk][j] = *reinterpret_cast<const v4i*>(smem + BO + offb[ks] + j * 32 * BK);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[kk][i] = *reinterpret_cast<const v4i*>(smem + BO + offa[ks] + i * 32 * BK);
+    }
+  };
+  auto mfma_seg = [&](int st, int q) {
+#pragma unroll
+    for (int kk = 0; kk < KPP; ++kk) {
+      v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
+      if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(s_mask + st * BK + 16 * (2 * (q * KPP + kk) + fh));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (QNN_ABLATE == 2) {
+            asm volatile("" ::"v"(fa[kk][i]), "v"(fb[kk][j]));
+            acc[i][j][0] += fa[kk][i].x;
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+          }
+          if (i == 0) {  // sum_valid(q'_x) of this column tile: one v_dot4 per MFMA gap
+            int s = __builtin_amdgcn_sdot4(fb[kk][j].x, ones.x, sumq[j], false);
+            s = __builtin_amdgcn_sdot4(fb[kk][j].y, ones.y, s, false);
+            s = __builtin_amdgcn_sdot4(fb[kk][j].z, ones.z, s, false);
+            sumq[j] = __builtin_amdgcn_sdot4(fb[kk][j].w, ones.w, s, false);
+          }
+        }
+    }
+  };
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+#if QNN_STAMP
+  const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  unsigned long long ts0 = 0, ts1 = 0;
+#endif
+  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed for every wave; waves 4-7
+  // then take one extra barrier (the stagger)
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) issue(0, 0, q);
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) issue(1, 1, q);
+  wait_vmcnt<P>();
+  bar();
+  if (late) bar();
+#if QNN_STAMP
+  QNN_TS(ts0);
+  const unsigned long long c_pro = ts0 - t_begin;
+#endif
+
+  auto ktile = [&](auto slotc, int st) {
+    constexpr int SL = decltype(slotc)::value;
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      read_frags(slotc, q);
+      issue(st + 2, (SL + 2) % NS, q);
+      if (q == PPT - 1) wait_vmcnt<P>();  // own DMA of K-tile st+1 landed (st+2 in flight)
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+      mfma_seg(st, q);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+  };
+  for (int st = 0; st < nstage; st += NS) {
+    ktile(std::integral_constant<int, 0>{}, st);
+    if (st + 1 < nstage) ktile(std::integral_constant<int, 1>{}, st + 1);
+    if (st + 2 < nstage) ktile(std::integral_constant<int, 2>{}, st + 2);
+    if (st + 3 < nstage) ktile(std::integral_constant<int, 3>{}, st + 3);
+  }
+  if (!late) bar();  // equal barrier counts
+  wait_vmcnt<0>();   // the clamped tail DMAs still write LDS
+#if QNN_STAMP
+  QNN_TS(ts1);
+  const unsigned long long c_loop = ts1 - ts0;
+#endif
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
+  __syncthreads();
+  if (QNN_ABLATE == 3) {
+    int z = sumq[0];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z ^= acc[i][j][r];
+    if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;
+    return;
+  }
+#if QNN_STAMP
+  QNN_TS(ts0);
+#endif
+  if (!p.epi_early) {  // no room beside the ring: stage into it now
+    stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+  epilogue<C, EK>(p, acc, sumq, pcls, smem, m0, c0, wm, wn, lane, tid, wave);
+#if QNN_STAMP
+  QNN_TS(ts1);
+  const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  unsigned hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  if (lane == 0 && blockIdx.x < (1 << 20) / (10 * W)) {
+    unsigned long long* o = qnn_dbg_stamps + ((size_t)blockIdx.x * W + wave) * 10;
+    o[0] = rt_start; o[1] = rt_end; o[2] = c_pro; o[3] = 0; o[4] = 0; o[5] = c_loop; o[6] = 0;
+    o[7] = ts1 - ts0; o[8] = hwid; o[9] = nstage;
+  }
+#endif
 }
 
-template <int BM, int BN, int BK, int EK, int TAPM, bool MASKED>
+template <class C>
+static int main_lds_bytes(int tapm, bool masked) {
+  return C::NS * C::STAGE + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
+}
+
+template <class C, int PP, int EK, int TAPM, bool MASKED>
 static int launch_kernel(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  auto kern = qconv_kernel<BM, BN, BK, EK, TAPM, MASKED>;
+  auto kern = [] {
+    if constexpr (PP > 0) return qconv_pp_kernel<C, PP, EK, TAPM, MASKED>;
+    else return qconv_kernel<C, EK, TAPM, MASKED>;
+  }();
   static const hipError_t attr =  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
-  const int lds_main = main_lds_bytes<BM, BN, BK>(TAPM, MASKED);
-  const int lds_epi = epi_lds_bytes(p.e, BM);
-  const int lds = lds_main > lds_epi ? lds_main : lds_epi;
-  const int nblk = (int)(cdiv(p.M, BN) * cdiv(p.d.cout, BM));
-  hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), lds, s, x, w, p);
+  // LDS: main-loop ring (+ tap table / K mask), epilogue data (early: beside the ring,
+  // late: at 0 once the ring is free), NCHW transpose scratch (after the loop)
+  constexpr int LDS_MAX = 160 * 1024;
+  const int lds_main = (main_lds_bytes<C>(TAPM, MASKED) + 15) & ~15;
+  const int k = epi_kind(p.e);
+  const int epi = 4 * (7 + p.e.nclass) * C::BM + (k == EK_LUT ? 256 * C::BM : 0);
+  const int scr = k == EK_NCHW ? 4096 * C::W : 0;
+  Params q = p;
+  int lds;
+  if (lds_main + epi <= LDS_MAX / C::BPC && scr <= lds_main) {
+    q.epi_early = 1, q.epi_off = lds_main, q.scr_off = 0;
+    lds = lds_main + epi;
+  } else {
+    q.epi_early = 0, q.epi_off = 0, q.scr_off = (epi + 15) & ~15;
+    lds = q.scr_off + scr > lds_main ? q.scr_off + scr : lds_main;
+  }
+  if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+  const int nblk = (int)(cdiv(p.M, C::BN) * cdiv(p.d.cout, C::BM));
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q);
   return QNN_OK;
 }
 
-template <int BM, int BN, int BK, int EK>
+template <class C, int PP, int EK>
 static int launch_tap(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  constexpr int CPR = BK / 16;
+  constexpr int CPR = C::CPR;
   const int cpt = 1 << p.lgcpt;
-  if (p.d.kmask) return launch_kernel<BM, BN, BK, EK, TAP_LDS, true>(x, w, p, s);
-  if (cpt >= CPR) return launch_kernel<BM, BN, BK, EK, TAP_ONE, false>(x, w, p, s);
-  if (2 * cpt == CPR) return launch_kernel<BM, BN, BK, EK, TAP_TWO, false>(x, w, p, s);
-  return launch_kernel<BM, BN, BK, EK, TAP_LDS, false>(x, w, p, s);
+  if (p.d.kmask) return launch_kernel<C, PP, EK, TAP_LDS, true>(x, w, p, s);
+  if (cpt >= CPR) return launch_kernel<C, PP, EK, TAP_ONE, false>(x, w, p, s);
+  if (2 * cpt == CPR) return launch_kernel<C, PP, EK, TAP_TWO, false>(x, w, p, s);
+  return launch_kernel<C, PP, EK, TAP_LDS, false>(x, w, p, s);
 }
 
-template <int BM, int BN, int BK>
+// PP = k-steps per ping-pong phase (qconv_pp_kernel), 0 = the plain ring loop (qconv_kernel)
+template <class C, int PP = 0>
 static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return launch_tap<BM, BN, BK, EK_NCHW>(x, w, p, s);
-    case EK_LUT: return launch_tap<BM, BN, BK, EK_LUT>(x, w, p, s);
-    case EK_BNCODE: return launch_tap<BM, BN, BK, EK_BNCODE>(x, w, p, s);
-    default: return launch_tap<BM, BN, BK, EK_GEN>(x, w, p, s);
+    case EK_NCHW: return launch_tap<C, PP, EK_NCHW>(x, w, p, s);
+    case EK_LUT: return launch_tap<C, PP, EK_LUT>(x, w, p, s);
+    case EK_BNCODE: return launch_tap<C, PP, EK_BNCODE>(x, w, p, s);
+    default:
+      // 256x256 blocks + the general chain spill registers: never picked, not built
+      if constexpr (C::TM * C::TN >= 8) return arg_error("general fused epilogue not built for this tile");
+      else return launch_tap<C, PP, EK_GEN>(x, w, p, s);
   }
 }
 
-// K-stage depth.  QNN_CONV_BK overrides (64 / 128) for A/B measurements.
-static int pick_bk(const Params& p) {
+// ---- tile configurations and the per-layer choice
+//   id  block (cout x px)  waves  LDS ring        blocks/CU  note
+//   0   256 x 256          8      4 x 32 KiB      1          1 byte from L2 per 256 ops
+//   1   128 x 256          8      4 x 24 KiB      1
+//   2   256 x 128          8      4 x 24 KiB      1
+//   3    64 x 256          4      4 x 20 KiB      2          64-channel layers
+//   4   128 x 128          4      4 x 16 KiB      2          small layers (more tiles)
+//   5    64 x 128          4      4 x 12 KiB      2          tiny layers / fc
+using C0 = Cfg<4, 2, 2, 4, 64, 4>;
+using C1 = Cfg<2, 4, 2, 2, 64, 4>;
+using C2 = Cfg<4, 2, 2, 2, 64, 4>;
+using C3 = Cfg<1, 4, 2, 2, 64, 4>;
+using C4 = Cfg<2, 2, 2, 2, 64, 4>;
+using C5 = Cfg<1, 2, 2, 2, 64, 4>;
+using C6 = Cfg<2, 4, 4, 2, 64, 4>;  // 256 x 256 ping-pong, waves 128 x 64, 1 k-step per phase
+using C7 = Cfg<2, 4, 2, 2, 64, 4>;  // 128 x 256 ping-pong, waves 64 x 64, 2 k-steps per phase
+using C8 = Cfg<4, 2, 2, 2, 64, 4>;  // 256 x 128 ping-pong
+using C10 = Cfg<1, 4, 2, 2, 64, 3, 2>;  // 64 x 256, 3-slot ring: 2 blocks/CU with a stem's K mask
+using C11 = Cfg<1, 4, 2, 1, 64, 3, 4>;  // 64 x 128, 3-slot ring: 4 blocks/CU (short-K, epilogue-bound layers)
+constexpr int NCFG = 12;  // 9: C6 with 2 k-steps per phase
+struct CfgInfo {
+  int bm, bn, per_cu;
+  float rate;  // relative MFMA throughput per CU (bytes moved per op, measured)
+};
+static const CfgInfo CFG[NCFG] = {
+    {256, 256, 1, 1.00f}, {128, 256, 1, 0.85f}, {256, 128, 1, 0.85f},
+    {64, 256, 2, 0.70f},  {128, 128, 2, 0.70f}, {64, 128, 2, 0.50f},
+    {256, 256, 1, 1.20f}, {128, 256, 1, 0.95f}, {256, 128, 1, 0.95f}, {256, 256, 1, 1.15f},
+    {64, 256, 2, 0.70f},  {64, 128, 4, 0.45f},
+};
+
+// Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
+// each round as long as one block's padded MFMA work at that config's rate.
+static double cfg_cost(int k, const Params& p) {
+  const CfgInfo& c = CFG[k];
+  const int64_t tiles = cdiv(p.M, c.bn) * cdiv(p.d.cout, c.bm);
+  const int64_t slots = (int64_t)NUM_CU * c.per_cu;
+  const int64_t rounds = cdiv(tiles, slots);
+  // with fewer tiles than slots the blocks of a round do not share a CU
+  const double share = tiles < slots ? (double)cdiv(tiles, NUM_CU) : (double)c.per_cu;
+  return (double)rounds * share * c.bm * c.bn * p.d.kpad / c.rate;
+}
+
+static int pick_cfg(const Params& p) {
   static int forced = [] {
-    const char* v = getenv("QNN_CONV_BK");
-    return v ? atoi(v) : 0;
+    const char* v = getenv("QNN_CONV_CFG");
+    return v ? atoi(v) : -1;
   }();
-  if (forced == 64 || forced == 128) return forced;
-  return p.d.cout <= 64 ? 64 : 128;
+  auto ok = [&](int k) { return k >= 0 && k < NCFG && !((k == 0 || k == 6 || k == 9) && epi_kind(p.e) == EK_GEN); };
+  if (ok(forced)) return forced;  // QNN_CONV_CFG: experiments override every caller
+  if (ok(p.d.tile - 1)) return p.d.tile - 1;
+  int best = -1;
+  double bc = 0;
+  for (int k = 0; k < NCFG; ++k) {
+    if (!ok(k)) continue;  // 256x256 + the general chain spills registers
+    const double c = cfg_cost(k, p);
+    if (best < 0 || c < bc) best = k, bc = c;
+  }
+  return best;
+}
+
+static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  switch (k) {
+    case 0: return launch_ek<C0>(x, w, p, s);
+    case 1: return launch_ek<C1>(x, w, p, s);
+    case 2: return launch_ek<C2>(x, w, p, s);
+    case 3: return launch_ek<C3>(x, w, p, s);
+    case 4: return launch_ek<C4>(x, w, p, s);
+    case 5: return launch_ek<C5>(x, w, p, s);
+    case 6: return launch_ek<C6, 1>(x, w, p, s);
+    case 7: return launch_ek<C7, 2>(x, w, p, s);
+    case 8: return launch_ek<C8, 2>(x, w, p, s);
+    case 9: return launch_ek<C6, 2>(x, w, p, s);
+    case 10: return launch_ek<C10>(x, w, p, s);
+    default: return launch_ek<C11>(x, w, p, s);
+  }
 }
 
 }  // namespace qnn
@@ -661,11 +1131,7 @@ extern "C" int qnn_debug_epi(void* dst, size_t bytes) {
 }
 #endif
 
-extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
-                               qnn_stream_t stream) {
-  QNN_REQUIRE(desc && epi, "null descriptor");
-  const qnn_conv_desc& d = *desc;
-  const qnn_epilogue& e = *epi;
+static int conv_params(const qnn_conv_desc& d, const qnn_epilogue& e, Params& p) {
   QNN_REQUIRE(d.n >= 0 && d.hp > 0 && d.wp > 0 && d.cout > 0 && d.kh > 0 && d.kw > 0 && d.sh > 0 && d.sw > 0,
               "bad shape");
   QNN_REQUIRE(d.cp >= 16 && (d.cp & (d.cp - 1)) == 0, "cp must be 16 * 2^j");
@@ -673,16 +1139,57 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   QNN_REQUIRE(d.ho > 0 && d.wo > 0 && (d.ho - 1) * d.sh + d.kh <= d.hp && (d.wo - 1) * d.sw + d.kw <= d.wp,
               "ho/wo exceed the padded input");
   QNN_REQUIRE(d.kpad % KPAD_ALIGN == 0 && d.kpad >= d.kh * d.kw * d.cp, "kpad must be a multiple of 128 covering K");
+  QNN_REQUIRE(d.cout_pad >= d.cout, "cout_pad < cout");
   QNN_REQUIRE((int64_t)d.n * d.hp * d.wp * d.cp < (1LL << 31) && d.zero_off >= 0 && d.zero_off % 16 == 0,
               "input too large or bad zero_off");
   QNN_REQUIRE(!d.kmask || (d.kpad <= MAX_MASK && (((uintptr_t)d.kmask) & 15) == 0), "kmask: kpad <= 1024, 16-B aligned");
   QNN_REQUIRE(e.nclass > 0 && e.nclass <= MAX_CLASSES && e.nwc > 0, "border classes out of range");
   QNN_REQUIRE(e.mode == 0 || e.mode == 1, "mode must be 0 (drop-in NCHW) or 1 (fused NHWC)");
+  p.d = d;
+  p.e = e;
+  const int64_t M = (int64_t)d.n * d.ho * d.wo;
+  QNN_REQUIRE(M < (1LL << 31), "too many output pixels");
+  p.M = (int)M;
+  p.taps = d.kh * d.kw;
+  p.lgcpt = __builtin_ctz(d.cp / 16);
+  p.kw_magic = (65536 + d.kw - 1) / d.kw;
+  p.ct = (int)cdiv(d.cout, 32);
+  static const int stagger = [] {
+    const char* v = getenv("QNN_CONV_STAGGER");
+    return v ? atoi(v) : 1;
+  }();
+  p.stagger = stagger;
+  return QNN_OK;
+}
+
+extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn,
+                             int* nblk) {
+  QNN_REQUIRE(desc && epi, "null descriptor");
+  Params p;
+  const int rc = conv_params(*desc, *epi, p);
+  if (rc != QNN_OK) return rc;
+  const int k = pick_cfg(p);
+  if (cfg) *cfg = k;
+  if (bm) *bm = CFG[k].bm;
+  if (bn) *bn = CFG[k].bn;
+  if (nblk) *nblk = (int)(cdiv(p.M, CFG[k].bn) * cdiv(p.d.cout, CFG[k].bm));
+  return QNN_OK;
+}
+
+extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
+                               qnn_stream_t stream) {
+  QNN_REQUIRE(desc && epi, "null descriptor");
+  const qnn_conv_desc& d = *desc;
+  const qnn_epilogue& e = *epi;
+  Params p;
+  const int rc0 = conv_params(d, e, p);
+  if (rc0 != QNN_OK) return rc0;
   if (d.n == 0) return QNN_OK;
   QNN_REQUIRE(x && wq && e.sxsw && e.sxbw && e.table && e.hcls && e.wcls, "null pointer");
   QNN_REQUIRE((((uintptr_t)x) & 15) == 0 && (((uintptr_t)wq) & 15) == 0, "x/wq must be 16-byte aligned");
   if (e.mode == 0) {
     QNN_REQUIRE(e.out_f32 != nullptr, "mode 0 needs out_f32");
+    QNN_REQUIRE((((uintptr_t)e.out_f32) & 15) == 0, "out_f32 must be 16-byte aligned");
   } else {
     QNN_REQUIRE(d.cout % 16 == 0, "fused mode needs cout % 16 == 0");
     QNN_REQUIRE(!e.bn_mean || (e.bn_sq && e.bn_wq && e.bn_bq && e.bn_scale > 0.f), "incomplete RangeBN");
@@ -699,22 +1206,8 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
     QNN_REQUIRE(!e.f32_tiled || ((((uintptr_t)e.out_f32) & 15) == 0 && (((uintptr_t)e.residual) & 15) == 0),
                 "C-tile fp32 maps must be 16-byte aligned");
   }
-  Params p;
-  p.d = d;
-  p.e = e;
-  const int64_t M = (int64_t)d.n * d.ho * d.wo;
-  QNN_REQUIRE(M < (1LL << 31), "too many output pixels");
-  p.M = (int)M;
-  p.taps = d.kh * d.kw;
-  p.lgcpt = __builtin_ctz(d.cp / 16);
-  p.kw_magic = (65536 + d.kw - 1) / d.kw;
-  p.ct = (int)cdiv(d.cout, 32);
   hipStream_t s = (hipStream_t)stream;
-  const bool narrow = d.cout <= 64;
-  QNN_REQUIRE(d.cout_pad >= (narrow ? 64 : 128) * (int)cdiv(d.cout, narrow ? 64 : 128), "cout_pad too small");
-  int rc;
-  if (narrow) rc = launch_ek<64, 256, 64>(x, wq, p, s);  // measured: BK=64 on 64-channel layers
-  else rc = pick_bk(p) == 128 ? launch_ek<128, 128, 128>(x, wq, p, s) : launch_ek<128, 128, 64>(x, wq, p, s);
+  const int rc = launch_cfg(pick_cfg(p), x, wq, p, s);
   if (rc != QNN_OK) return rc;
   QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
   return QNN_OK;

@@ -137,33 +137,42 @@ __global__ void quantize_nchw_nhwc8_kernel(const float* __restrict__ x, int8_t* 
     *reinterpret_cast<int4*>(q + npix * cp + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
-// Space-to-depth codes (factor 2): z[n][h2][w2][(2u+v)*c + ci], 16 channels.
-__global__ void quantize_s2d_kernel(const float* __restrict__ x, int8_t* __restrict__ z, int n, int c, int h, int w,
-                                    int pad, int hz, int wz, float neg_min, float scale, float qmax) {
-  const int64_t npix = (int64_t)n * hz * wz;
-  for (int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pix < npix;
-       pix += (int64_t)gridDim.x * blockDim.x) {
-    const int w2 = (int)(pix % wz);
-    const int64_t t = pix / wz;
-    const int h2 = (int)(t % hz);
-    const int64_t img = t / hz;
-    union {
-      int8_t b[16];
-      int4 v;
-    } out;
-    out.v = make_int4(0, 0, 0, 0);
-#pragma unroll
-    for (int uv = 0; uv < 4; ++uv) {
-      const int iy = 2 * h2 + (uv >> 1) - pad, ix = 2 * w2 + (uv & 1) - pad;
-      if (iy < 0 || iy >= h || ix < 0 || ix >= w) continue;
-      const float* src = x + (img * c) * (int64_t)h * w + (int64_t)iy * w + ix;
-      for (int ci = 0; ci < c; ++ci)
-        out.b[uv * c + ci] = (int8_t)((int)quant_code(src[(int64_t)ci * h * w], neg_min, scale, qmax) - 128);
+// Space-to-depth codes (factor 2): z[n][h2][w2][(2u+v)*c + ci], 16 channels.  One block per
+// (image, s2d row): the 2*c input rows it needs are read coalesced (consecutive lanes =
+// consecutive x), quantized (quant_code_fast == IEEE division, bit for bit) into LDS, then
+// every thread assembles whole 16-byte s2d pixels.
+__global__ __launch_bounds__(256) void quantize_s2d_kernel(const float* __restrict__ x, int8_t* __restrict__ z, int n,
+                                                           int c, int h, int w, int pad, int hz, int wz, float neg_min,
+                                                           float scale, float qmax) {
+  extern __shared__ int8_t s_rows[];  // [2][c][2*wz] codes'
+  const int row = blockIdx.x, img = row / hz, h2 = row - img * hz;
+  const int W2 = 2 * wz, per_u = c * W2;
+  const float inv = 1.0f / scale;
+  if (n > 0) {
+    for (int i = threadIdx.x; i < 2 * per_u; i += blockDim.x) {
+      const int u = i / per_u, rem = i - u * per_u, ci = rem / W2, xx = rem - ci * W2;
+      const int iy = 2 * h2 + u - pad, ix = xx - pad;
+      int8_t v = 0;
+      if (iy >= 0 && iy < h && ix >= 0 && ix < w)
+        v = (int8_t)((int)quant_code_fast(x[(((int64_t)img * c + ci) * h + iy) * w + ix], neg_min, scale, inv, qmax) -
+                     128);
+      s_rows[i] = v;
     }
-    *reinterpret_cast<int4*>(z + pix * 16) = out.v;
+    __syncthreads();
+    for (int w2 = threadIdx.x; w2 < wz; w2 += blockDim.x) {
+      union {
+        int8_t b[16];
+        int4 v;
+      } out;
+      out.v = make_int4(0, 0, 0, 0);
+#pragma unroll
+      for (int uv = 0; uv < 4; ++uv)
+        for (int ci = 0; ci < c; ++ci) out.b[uv * c + ci] = s_rows[((uv >> 1) * c + ci) * W2 + 2 * w2 + (uv & 1)];
+      *reinterpret_cast<int4*>(z + ((int64_t)row * wz + w2) * 16) = out.v;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x < 8)
-    *reinterpret_cast<int4*>(z + npix * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
+    *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
 // ------------------------------------------------------------------ weight pack
@@ -417,9 +426,9 @@ int qnn_quantize_nchw_to_s2d8(const float* x, int8_t* z, int n, int c, int h, in
   QNN_REQUIRE(scale > 0.f, "scale must be > 0");
   QNN_REQUIRE(z && (n == 0 || x), "null pointer");
   QNN_REQUIRE((((uintptr_t)z) & 15) == 0, "z must be 16-byte aligned");
-  int64_t work = (int64_t)n * hz * wz;
-  hipLaunchKernelGGL(quantize_s2d_kernel, dim3(grid_for(work > 0 ? work : 1, 256)), dim3(256), 0, (hipStream_t)stream,
-                     x, z, n, c, h, w, pad, hz, wz, neg_min, scale, qmax);
+  const int64_t rows = (int64_t)n * hz;
+  hipLaunchKernelGGL(quantize_s2d_kernel, dim3((unsigned)(rows > 0 ? rows : 1)), dim3(256), 2 * c * 2 * wz,
+                     (hipStream_t)stream, x, z, n, c, h, w, pad, hz, wz, neg_min, scale, qmax);
   QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_s2d8");
   return QNN_OK;
 }

@@ -69,7 +69,7 @@ class Engine:
     the model's device).  `engine.input` is a static input buffer; passing it (or
     nothing) avoids the copy.  graph=False runs the launches eagerly (debugging)."""
 
-    def __init__(self, model, batch, input_hw=None, graph=True):
+    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True):
         if model.training:
             raise RuntimeError("qnn.Engine: call model.eval() first (the engine is the eval forward)")
         self.model = model
@@ -81,6 +81,7 @@ class Engine:
         self.ops = []
         self.keep = []
         self.launch_names = []
+        self.convs = []  # (op index, ConvDesc, Epilogue) of every contraction
         with torch.no_grad():
             if hasattr(model, "features") and hasattr(model, "fc"):
                 hw = input_hw or 224
@@ -90,6 +91,9 @@ class Engine:
                 self._plan_resnet(model, hw)
             else:
                 raise NotImplementedError("qnn.Engine supports resnet_quantized and mobilenet_quantized models")
+        self.tiles = None
+        if autotune:
+            self._autotune()
         self.graph = None
         if graph:
             self._capture()
@@ -196,6 +200,7 @@ class Engine:
         xbuf = src[1] if s2d else src[0]
         self.keep += [pk, sxsw, sxbw, table, g, d, e, xbuf]
         xp, wp_, dp, ep = _lib.ptr(xbuf), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e)
+        self.convs.append((len(self.ops), d, e))
         self._add("qnn_qconv2d_fwd", lambda st: _lib.call("qnn_qconv2d_fwd", xp, wp_, dp, ep, st))
         return Ho, Wo
 
@@ -420,6 +425,37 @@ class Engine:
         self._plan_head(model, x, model.avg_pool.kernel_size)
 
     # ------------------------------------------------------------------ execution
+    def _autotune(self, reps=3):
+        """Pick each contraction's tile configuration by timing every one on this device
+        (HIP events on the launch stream).  Every configuration computes the identical
+        result, so this only changes speed.  Runs the launch list once first so every
+        buffer a conv reads holds real data; re-running a conv is idempotent."""
+        st = _lib.stream_of(self.input)
+        with torch.no_grad():
+            self._run_ops()
+            self.tiles = []
+            for idx, d, _e in self.convs:
+                op = self.ops[idx]
+                best = None
+                for k in range(_lib.CONV_TILES):
+                    d.tile = k + 1
+                    try:
+                        op(st)
+                    except _lib.QnnError:
+                        continue  # configuration not built for this epilogue
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(reps):
+                        op(st)
+                    e1.record()
+                    e1.synchronize()
+                    ms = e0.elapsed_time(e1) / reps
+                    if best is None or ms < best[1]:
+                        best = (k, ms)
+                d.tile = best[0] + 1
+                self.tiles.append(best)
+            torch.cuda.synchronize(self.dev)
+
     def _run_ops(self):
         st = _lib.stream_of(self.input)  # the current stream (the capture stream while capturing)
         for op in self.ops:

@@ -437,6 +437,7 @@ class _QLayerMixin:
         e.bias = None if pk.qbias is None else pk.qbias.data_ptr()
         e.out_f32 = y.data_ptr()
         _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
+        self._last_conv = (d, e)  # launch descriptors, for profiling tools (qnn_conv_plan)
         return y
 
 

@@ -27,16 +27,27 @@ from qnn import _lib  # noqa: E402
 NF = 10
 
 
-def read(nblk):
+def plan(d, e=None):
+    """(cfg, waves per block, blocks) of the conv launch for descriptor d."""
+    cfg, bm, bn, nblk = (ctypes.c_int() for _ in range(4))
+    e = e if e is not None else _lib.Epilogue(mode=1)
+    _lib.call("qnn_conv_plan", ctypes.byref(d), ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(bm),
+              ctypes.byref(bn), ctypes.byref(nblk))
+    waves = 8 if cfg.value in (0, 1, 2) else 4
+    return cfg.value, waves, nblk.value
+
+
+def read(nblk, W):
     lib = _lib.load()
     fn, fe = lib.qnn_debug_stamps, lib.qnn_debug_epi
     fn.argtypes = fe.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    buf = np.zeros(nblk * 4 * NF, dtype=np.uint64)
-    ebuf = np.zeros(nblk * 4 * 4, dtype=np.uint64)
+    nblk = min(nblk, (1 << 20) // (10 * W), (1 << 18) // (4 * W))
+    buf = np.zeros(nblk * W * NF, dtype=np.uint64)
+    ebuf = np.zeros(nblk * W * 4, dtype=np.uint64)
     torch.cuda.synchronize()
     assert fn(buf.ctypes.data, buf.nbytes) == 0
     assert fe(ebuf.ctypes.data, ebuf.nbytes) == 0
-    return buf.reshape(nblk, 4, NF), ebuf.reshape(nblk, 4, 4)
+    return buf.reshape(nblk, W, NF), ebuf.reshape(nblk, W, 4)
 
 
 def report(tag, sts):
@@ -45,7 +56,7 @@ def report(tag, sts):
     w = st.astype(np.float64)
     cyc = w[:, :, 2:8]
     tot = cyc.sum(-1)
-    names = ["prologue", "issue", "wait+bar", "compute", "bar2", "epilogue"]
+    names = ["prologue", "issue", "wait+bar", "compute", "-", "epilogue"]
     mean = cyc.mean((0, 1))
     print(f"== {tag}: blocks={nblk} stages={int(w[0, 0, 9])} wave-cycles mean={tot.mean():.0f} "
           f"(min {tot.min():.0f} max {tot.max():.0f})")
@@ -94,12 +105,8 @@ def main():
             with torch.no_grad():
                 for _ in range(3):
                     wrap(x)
-            Ho = (H + 2 * pd - k) // stv + 1
-            M = N * Ho * Ho
-            bn_ = 256 if cout <= 64 else 128
-            bm_ = 64 if cout <= 64 else 128
-            nblk = -(-M // bn_) * -(-cout // bm_)
-            report(name, read(nblk))
+            cfg_, W, nblk = plan(*m._last_conv)
+            report(f"{name} cfg={cfg_}", read(nblk, W))
     if a.engine:
         import bench
         from qnn import synthetic
@@ -108,6 +115,7 @@ def main():
         eng = Engine(model, batch=128, graph=False)
         eng.input.copy_(synthetic.input_batch((128, 3, 224, 224), 1234).to(dev))
         descs = [k for k in eng.keep if isinstance(k, _lib.ConvDesc)]
+        epis = [k for k in eng.keep if isinstance(k, _lib.Epilogue)]
         st = _lib.stream_of(eng.input)
         with torch.no_grad():
             eng()
@@ -116,15 +124,13 @@ def main():
                 op(st)
                 if name != "qnn_qconv2d_fwd":
                     continue
-                d = descs[ci]
+                d, e = descs[ci], epis[ci]
                 ci += 1
                 if i not in a.engine:
                     continue
                 M = d.n * d.ho * d.wo
-                bn_ = 256 if d.cout <= 64 else 128
-                bm_ = 64 if d.cout <= 64 else 128
-                nblk = -(-M // bn_) * -(-d.cout // bm_)
-                report(f"engine launch {i} M={M} cout={d.cout} K={d.kh * d.kw * d.cp}", read(nblk))
+                cfg_, W, nblk = plan(d, e)
+                report(f"engine launch {i} M={M} cout={d.cout} K={d.kh * d.kw * d.cp} cfg={cfg_}", read(nblk, W))
 
 
 if __name__ == "__main__":
