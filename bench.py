@@ -73,39 +73,63 @@ def calibrate(model, device, seed, batches=2, bsz=16):
     model.eval()
 
 
-def build(device, depth, seed=11):
+def build(device, depth, seed=11, arch="resnet"):
     from qnn import synthetic
-    from qnn.resnet_quantized import resnet_quantized
     torch.manual_seed(0)
-    model = resnet_quantized(depth=depth, dataset="imagenet")
+    if arch == "mobilenet":
+        from qnn.mobilenet_quantized import mobilenet_quantized
+        model = mobilenet_quantized()
+    else:
+        from qnn.resnet_quantized import resnet_quantized
+        model = resnet_quantized(depth=depth, dataset="imagenet")
     synthetic.init_params(model, seed)
     model = model.to(device)
     calibrate(model, device, 300)
     return model
 
 
-def cpu_baseline(model_cpu_sd, depth, batch, iters, threads):
+def cpu_baseline(model_cpu_sd, depth, batch, iters, threads, arch="resnet"):
     """Oracle (the reference's fake-quant CPU forward, restated) on a bounded sample."""
     from oracle import qnn_oracle as O
     from qnn import synthetic
     torch.set_num_threads(threads)
     x = synthetic.input_batch((batch, 3, 224, 224), 4242)
     sd = {k: v.clone() for k, v in model_cpu_sd.items()}
-    kw = dict(depth=depth, dataset="imagenet")
-    O.model_forward(sd, x, "resnet", kw)  # warm-up
+    kw = dict(depth=depth, dataset="imagenet") if arch == "resnet" else {}
+    O.model_forward(sd, x, arch, kw)  # warm-up
     times = []
     t_end = time.perf_counter() + 30.0
     for _ in range(iters):
         t0 = time.perf_counter()
-        O.model_forward(sd, x, "resnet", kw)
+        O.model_forward(sd, x, arch, kw)
         times.append(time.perf_counter() - t0)
         if time.perf_counter() > t_end:
             break
     med = float(np.median(times))
     return {"value": round(batch / med, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/qnn_oracle.py resnet{depth} imagenet fake-quant forward (biprecision double conv, "
+            "sample": f"oracle/qnn_oracle.py {model_name(arch, depth)} imagenet fake-quant forward (biprecision double conv, "
                       f"as the reference), batch {batch}, median of {len(times)} after 1 warm-up, "
                       f"torch {torch.__version__} CPU, {threads} threads, {platform.processor() or platform.machine()}"}
+
+
+def model_name(arch, depth):
+    return "mobilenet" if arch == "mobilenet" else f"resnet{depth}"
+
+
+def pmc_traffic(arch, depth, batch):
+    """HBM bytes per forward of the conv launches, from the committed rocprofv3 PMC passes of
+    this workload (tools/traffic.py: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE).
+    None when no summary for this exact workload is committed."""
+    import glob
+    import re
+    paths = glob.glob(os.path.join(HERE, "profiles", f"r*_traffic_{model_name(arch, depth)}_b{batch}.json"))
+    if not paths:
+        return None
+    latest = max(paths, key=lambda p: int(re.search(r"r(\d+)_traffic", os.path.basename(p)).group(1)))
+    with open(latest) as f:
+        d = json.load(f)
+    d["source"] = f"profiles/{os.path.basename(latest)}: " + d["source"]
+    return d
 
 
 def main():
@@ -115,6 +139,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--depth", type=int, default=18)
+    ap.add_argument("--model", choices=("resnet", "mobilenet"), default="resnet")
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-iters", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -130,7 +155,7 @@ def main():
     torch.cuda.set_device(device)
     _lib.load()
 
-    model = build(device, args.depth)
+    model = build(device, args.depth, arch=args.model)
     total_ops, mfma_ops = model_ops(model, args.batch)
     from qnn import synthetic
     from qnn.engine import Engine
@@ -195,6 +220,8 @@ def main():
         images = args.batch * world * args.steps
         ms_per_step = elapsed / args.steps * 1e3
         achieved = mfma_ops / (conv_ms_per_fwd * 1e-3) / 1e12
+        pmc = pmc_traffic(args.model, args.depth, args.batch)
+        nconv = sum(1 for n in engine.launch_names if n == "qnn_qconv2d_fwd")
         line = {
             "metric": METRIC,
             "value": round(images / elapsed, 2),
@@ -208,13 +235,16 @@ def main():
             "vs_baseline": None,
             "dtype": "int8",
             "data": "synthetic (N(0,1) 3x224x224 on device; numpy-PCG64 weights, reference init law)",
-            "config": {"workload": f"resnet_quantized depth={args.depth} imagenet eval forward, fused int8 engine "
+            "config": {"workload": (f"resnet_quantized depth={args.depth}" if args.model == "resnet" else
+                                    "mobilenet_quantized") + f" imagenet eval forward, fused int8 engine "
                                    f"(hipGraph), per-GPU batch {args.batch}",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "model_gop_per_batch": round(total_ops / 1e9, 2)},
-            "roofline": {"bound": "mfma", "kernel": "qconv_kernel (all 21 QConv2d/QLinear launches of one forward)",
+            "roofline": {"bound": "mfma", "kernel": f"qconv_kernel (all {nconv} QConv2d/QLinear launches of one forward)",
                          "achieved": round(achieved, 2), "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_INT8_TOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_INT8_TOPS, 4),
+                         "traffic": None if pmc is None else pmc["hbm_bytes_per_forward"],
+                         "traffic_source": None if pmc is None else pmc["source"],
                          "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
                          "model_frac": round(total_ops / (ms_per_step * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4)},
             "engine": {"launches_per_forward": launches, "hipgraph": True,
@@ -225,7 +255,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, len(os.sched_getaffinity(0)))
             sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-            line["cpu_baseline"] = cpu_baseline(sd, args.depth, args.cpu_batch, args.cpu_iters, threads)
+            line["cpu_baseline"] = cpu_baseline(sd, args.depth, args.cpu_batch, args.cpu_iters, threads,
+                                                arch=args.model)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

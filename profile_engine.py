@@ -25,12 +25,13 @@ from qnn.engine import Engine  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--depth", type=int, default=18)
+    ap.add_argument("--model", choices=("resnet", "mobilenet"), default="resnet")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     _lib.load()
-    model = bench.build(dev, a.depth)
+    model = bench.build(dev, a.depth, arch=a.model)
     eng = Engine(model, batch=a.batch, graph=False)
     eng.input.copy_(synthetic.input_batch((a.batch, 3, 224, 224), 1234).to(dev))
     descs = [k for k in eng.keep if isinstance(k, _lib.ConvDesc)]
@@ -59,7 +60,13 @@ def main():
             M = c.n * c.ho * c.wo
             K = c.kh * c.kw * c.cp
             ops = 2 * M * c.cout * K
-            row.update(MxNxK=[M, c.cout, K], cfg=cfg.value, tile=[bm.value, bn.value], blocks=nb.value, tops=round(ops / ms / 1e9, 1), frac=round(ops / ms / 1e9 / 5000, 4))
+            e = epis[ci - 1]
+            # algorithmic bytes: the padded input codes + packed weights + every output written
+            # (fp32 4 B/elem, codes 1 B/elem per consumer, RangeBN codes 1 B; + fp32 residual read)
+            out_b = M * c.cout * ((4 if e.out_f32 else 0) + (1 if e.out_code0 else 0) + (1 if e.out_code1 else 0)
+                                 + (1 if e.out_bncode else 0) + (4 if e.residual else 0))
+            alg = c.n * c.hp * c.wp * c.cp + c.cout * c.kpad + out_b
+            row.update(MxNxK=[M, c.cout, K], alg_bytes=alg, cfg=cfg.value, tile=[bm.value, bn.value], blocks=nb.value, tops=round(ops / ms / 1e9, 1), frac=round(ops / ms / 1e9 / 5000, 4))
         rows.append(row)
         print(json.dumps(row), flush=True)
     tot = sum(r["us"] for r in rows)

@@ -27,6 +27,7 @@ therefore applied once, not per forward).  Rebuild the engine after changing
 weights or calibration.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -92,7 +93,15 @@ class Engine:
             else:
                 raise NotImplementedError("qnn.Engine supports resnet_quantized and mobilenet_quantized models")
         self.tiles = None
-        if autotune:
+        fixed = os.environ.get("QNN_ENGINE_TILES")  # "k,k,..." per contraction (reproducible profiles)
+        if fixed:
+            ks = [int(v) for v in fixed.split(",")]
+            if len(ks) != len(self.convs):
+                raise ValueError(f"QNN_ENGINE_TILES has {len(ks)} entries, the plan has {len(self.convs)} convs")
+            for (_i, d, _e), k in zip(self.convs, ks):
+                d.tile = k + 1
+            self.tiles = [(k, None) for k in ks]
+        elif autotune:
             self._autotune()
         self.graph = None
         if graph:
