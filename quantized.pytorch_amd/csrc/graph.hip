@@ -1,7 +1,10 @@
 // Fused model-graph kernels around the int8 contraction (HBM-bound, NHWC, coalesced
 // along channels, 4 channels per thread): code-domain max-pool, fused depthwise conv,
 // avg-pool head.  Reference semantics cited per entry in include/qnn.h.
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include "qnn_internal.h"
 
@@ -185,6 +188,139 @@ __global__ void dwconv_fused_kernel(const int8_t* __restrict__ x, int n, int h, 
   }
 }
 
+// Depthwise 3x3 (MobileNet's every depthwise layer), same arithmetic op for op as
+// dwconv_fused_kernel (so bitwise equal to it and to the module path): each tap's
+// x_hat = fl(fl(q*s)+min), fmaf into the accumulator in (r, s) row-major order with
+// out-of-image taps skipped, + bias, RangeBN on its quantized input, ReLU, the
+// consumer's codes.  Layout of the work instead: a thread owns 8 channels (8-byte
+// loads, coalesced along channels across the ct = c/8 channel threads) of R
+// consecutive output pixels of one row, so each input column is dequantized once
+// and feeds up to 3 outputs from registers; the 9x8 tap weights, the bias and the
+// RangeBN vectors live in registers; both quantizers run division-free
+// (quant_code_fast, bit-identical); no 64-bit index arithmetic.
+template <int S, int R>
+__global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__ x, int h, int w, int pad, int hp,
+                                                      int wp, int cp, int c, const float* __restrict__ wt, int ho,
+                                                      int wo, float x_min, float x_scale, const float* bias,
+                                                      qnn_bn_params bn, float bn_inv, int has_bn, int relu,
+                                                      float* out_f32, qnn_code_out c0, float c0_inv, int rows) {
+  constexpr int K = 3, NCOL = (R - 1) * S + K;
+  const int ct = c >> 3, per_blk = 256 / ct;
+  const int tc = threadIdx.x % ct, tp = threadIdx.x / ct;
+  if (tp >= per_blk) return;  // c/8 not a divisor of 256: idle tail threads
+  const int nxg = (wo + R - 1) / R, total = rows * nxg, cb = 8 * tc;
+  if (blockIdx.x * per_blk + tp >= total) return;
+  float wv[K * K][8];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) {
+    const float4 a = *reinterpret_cast<const float4*>(wt + t * c + cb);
+    const float4 b = *reinterpret_cast<const float4*>(wt + t * c + cb + 4);
+    wv[t][0] = a.x, wv[t][1] = a.y, wv[t][2] = a.z, wv[t][3] = a.w;
+    wv[t][4] = b.x, wv[t][5] = b.y, wv[t][6] = b.z, wv[t][7] = b.w;
+  }
+  float bi[8], mean[8], sq[8], wq[8], bq[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    bi[u] = bias ? bias[cb + u] : 0.f;
+    if (has_bn) mean[u] = bn.mean[cb + u], sq[u] = bn.sq[cb + u], wq[u] = bn.wq[cb + u], bq[u] = bn.bq[cb + u];
+  }
+  // Every load unconditional (clamped in-buffer addresses: the padded buffer holds any row
+  // oy*S + r and column < wp) and all K x NCOL issued together -- a load under a branch
+  // gets its own vmcnt(0) wait.  Software-pipelined: the next group's loads are in flight
+  // while this group computes.
+  auto load = [&](int g, uint2 (&v)[K][NCOL]) {
+    const int row = g / nxg, xg = g - row * nxg;
+    const int img = row / ho, oy = row - img * ho;
+    const int8_t* xrow = x + ((size_t)img * hp + oy * S) * wp * cp + cb;
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+      for (int col = 0; col < NCOL; ++col) {
+        const int px = min(xg * R * S + col, wp - 1);
+        v[r][col] = *reinterpret_cast<const uint2*>(xrow + ((size_t)r * wp + px) * cp);
+      }
+  };
+  // grid-stride over (row, R-pixel group): the register-resident parameters are loaded
+  // once per thread and reused across all of its groups
+  const int step = gridDim.x * per_blk;
+  uint2 v[K][NCOL];
+  load(blockIdx.x * per_blk + tp, v);
+  for (int pg = blockIdx.x * per_blk + tp; pg < total; pg += step) {
+    const int row = pg / nxg, xg = pg - row * nxg;
+    const int img = row / ho, oy = row - img * ho;
+    const int ox0 = xg * R;
+    uint2 vn[K][NCOL];
+    load(min(pg + step, total - 1), vn);
+    float acc[R][8];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[j][u] = 0.f;
+
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int py = oy * S + r;
+      if (py < pad || py >= pad + h) continue;  // uniform over the pixel group
+#pragma unroll
+      for (int col = 0; col < NCOL; ++col) {
+        const int px = ox0 * S + col;
+        if (px < pad || px >= pad + w) continue;
+        const uint32_t lo = v[r][col].x ^ 0x80808080u, hi = v[r][col].y ^ 0x80808080u;  // code' ^ 0x80 = code
+        float xh[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          xh[u] = dequant((float)((lo >> (8 * u)) & 255), x_scale, x_min);
+          xh[4 + u] = dequant((float)((hi >> (8 * u)) & 255), x_scale, x_min);
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const int s = col - j * S;
+          if (s < 0 || s >= K) continue;  // compile-time
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc[j][u] = fmaf(xh[u], wv[r * K + s][u], acc[j][u]);
+        }
+      }
+    }
+
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int ox = ox0 + j;
+      if (ox >= wo) break;
+      float val[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float y = bias ? acc[j][u] + bi[u] : acc[j][u];
+        if (has_bn) {
+          const float q = quant_code_fast(y, bn.neg_min, bn.scale, bn_inv, bn.qmax);
+          float o = dequant(q, bn.scale, bn.min) - mean[u];  // bn_apply, quantize.py:488-499
+          o = o * sq[u];
+          o = o * wq[u];
+          y = o + bq[u];
+        }
+        val[u] = relu ? fmaxf(y, 0.f) : y;
+      }
+      if (out_f32) {
+        float* o = out_f32 + (((size_t)img * ho + oy) * wo + ox) * c + cb;
+        *reinterpret_cast<float4*>(o) = make_float4(val[0], val[1], val[2], val[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(val[4], val[5], val[6], val[7]);
+      }
+      if (c0.ptr) {
+        uint32_t p[2] = {0u, 0u};
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          p[u >> 2] |= (uint32_t)(((int)quant_code_fast(val[u], c0.neg_min, c0.scale, c0_inv, c0.qmax) - 128) & 255)
+                       << (8 * (u & 3));
+        *reinterpret_cast<uint2*>(c0.ptr + (((size_t)img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * c0.cp + cb) =
+            make_uint2(p[0], p[1]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+      for (int col = 0; col < NCOL; ++col) v[r][col] = vn[r][col];
+  }
+}
+
 // ------------------------------------------------------------------ RangeBN -> code LUT
 __global__ void bn_code_lut_kernel(qnn_bn_params bn, int c, int relu, qnn_code_out nx, int8_t* lut) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -297,6 +433,30 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
   memset(&b, 0, sizeof(b));
   if (bn) b = *bn;
   const qnn_code_out c0 = code0 ? *code0 : none_code();
+  const char* fg = getenv("QNN_DW_GENERIC");  // read per call: tests compare both kernels bitwise
+  const int force_generic = fg ? atoi(fg) : 0;
+  const bool fast = !force_generic && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) && c % 8 == 0 &&
+                    c / 8 <= 256 && cp % 8 == 0 && (((uintptr_t)x) & 7) == 0 && (((uintptr_t)w_hat_t) & 15) == 0 &&
+                    (!out_f32 || (((uintptr_t)out_f32) & 15) == 0) &&
+                    (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0));
+  if (fast) {
+    const int R = sh == 1 ? 4 : 2;  // stride 2: 2 pixels (5 input columns) per thread, register budget
+    const int rows = n * ho, ct = c / 8;
+    const int64_t groups = (int64_t)rows * ((wo + R - 1) / R);
+    QNN_REQUIRE(groups < (1LL << 31) && (int64_t)n * hp * wp * cp < (1LL << 40), "depthwise too large");
+    auto kern = sh == 1 ? dwconv3_kernel<1, 4> : dwconv3_kernel<2, 2>;
+    // grid-stride, sized to the resident capacity (the loop is software-pipelined)
+    static int num_cu = 0;
+    if (!num_cu && hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) num_cu = 256;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int blocks = (int)std::min<int64_t>(cdiv(groups, 256 / ct), (int64_t)num_cu * per_cu);
+    const float bn_inv = bn ? 1.0f / b.scale : 1.0f, c0_inv = c0.ptr ? 1.0f / c0.scale : 1.0f;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, h, w, pad, hp, wp, cp, c, w_hat_t,
+                       ho, wo, x_min, x_scale, bias, b, bn_inv, bn ? 1 : 0, relu, out_f32, c0, c0_inv, rows);
+    QNN_LAUNCH_CHECK("qnn_dwconv_fused");
+    return QNN_OK;
+  }
   hipLaunchKernelGGL(dwconv_fused_kernel, dim3(grid_for((int64_t)n * ho * wo * (c / 4))), dim3(256), 0,
                      (hipStream_t)stream, x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min,
                      x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0);
