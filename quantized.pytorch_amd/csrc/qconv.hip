@@ -176,16 +176,24 @@ static inline int epi_kind(const qnn_epilogue& e) {
 
 // y for channels cl..cl+3 (register group g of an accumulator): the exact decomposition
 // s_x*s_w*acc + s_x*b_w*sum_valid(q'_x) + border term, + bias; parameters read as float4.
-__device__ __forceinline__ void conv_out4(const float* s_f, int BM, int cl, int ptab, float psq, const v16i& a, int g,
-                                          float (&v)[4]) {
+// Packed pairs: v[0] = channels cl, cl+1; v[1] = cl+2, cl+3 (fma(sw, acc, fma(bw, psq, tb)) + bias).
+__device__ __forceinline__ void conv_out4p(const float* s_f, int BM, int cl, int ptab, float psq, const v16i& a, int g,
+                                           f2 (&v)[2]) {
   const float4 sw = *reinterpret_cast<const float4*>(s_f + cl);
   const float4 bw = *reinterpret_cast<const float4*>(s_f + BM + cl);
   const float4 tb = *reinterpret_cast<const float4*>(s_f + ptab + cl);
   const float4 bi = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
-  v[0] = fmaf(sw.x, (float)a[4 * g + 0], fmaf(bw.x, psq, tb.x)) + bi.x;
-  v[1] = fmaf(sw.y, (float)a[4 * g + 1], fmaf(bw.y, psq, tb.y)) + bi.y;
-  v[2] = fmaf(sw.z, (float)a[4 * g + 2], fmaf(bw.z, psq, tb.z)) + bi.z;
-  v[3] = fmaf(sw.w, (float)a[4 * g + 3], fmaf(bw.w, psq, tb.w)) + bi.w;
+  const f2 p2 = {psq, psq};
+  const f2 a01 = {(float)a[4 * g + 0], (float)a[4 * g + 1]}, a23 = {(float)a[4 * g + 2], (float)a[4 * g + 3]};
+  v[0] = pfma((f2){sw.x, sw.y}, a01, pfma((f2){bw.x, bw.y}, p2, (f2){tb.x, tb.y})) + (f2){bi.x, bi.y};
+  v[1] = pfma((f2){sw.z, sw.w}, a23, pfma((f2){bw.z, bw.w}, p2, (f2){tb.z, tb.w})) + (f2){bi.z, bi.w};
+}
+
+__device__ __forceinline__ void conv_out4(const float* s_f, int BM, int cl, int ptab, float psq, const v16i& a, int g,
+                                          float (&v)[4]) {
+  f2 p[2];
+  conv_out4p(s_f, BM, cl, ptab, psq, a, g, p);
+  v[0] = p[0].x, v[1] = p[0].y, v[2] = p[1].x, v[3] = p[1].y;
 }
 
 // Epilogue data in LDS at p.epi_off (f32 unless noted):
@@ -337,7 +345,10 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
       }
     }
   } else {
-    const float bn_inv = 1.0f / e.bn_scale, c0_inv = 1.0f / e.code0_scale, c1_inv = 1.0f / e.code1_scale;
+    const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+    const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
+    const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+    const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
     const CodeDst t0 = {e.out_code0, e.code0_cp, e.code0_pad, e.code0_hp, e.code0_wp};
     const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
     const CodeDst tb = {reinterpret_cast<int8_t*>(e.out_bncode), d.cout, 0, d.ho, d.wo};
@@ -371,27 +382,26 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
           const int cl = cb - c0 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
           const int c = c0 + cl;
           const bool cok = c < d.cout;  // cout % 16 == 0: a 4-channel group is all in or all out
-          float v[4];
-          conv_out4(s_f, BM, cl, ptab[j], psq[j], acc[i][j], g, v);
+          f2 v[2];
+          conv_out4p(s_f, BM, cl, ptab[j], psq[j], acc[i][j], g, v);
           k0[g] = k1[g] = 0;
           if constexpr (EK == EK_LUT) {  // conv -> RangeBN -> ReLU -> next quantizer, tabulated (exact)
+            const f2 m0 = qclamp2(v[0], bnp) + MAGIC_U8, m1 = qclamp2(v[1], bnp) + MAGIC_U8;
+            const unsigned qq[4] = {__float_as_uint(m0.x) & 255u, __float_as_uint(m0.y) & 255u,
+                                    __float_as_uint(m1.x) & 255u, __float_as_uint(m1.y) & 255u};
             int r = 0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int q = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);
-              r |= ((int)(uint8_t)s_tail[(cl + u) * 256 + q]) << (8 * u);
-            }
+            for (int u = 0; u < 4; ++u) r |= ((int)(uint8_t)s_tail[(cl + u) * 256 + qq[u]]) << (8 * u);
             k0[g] = cok ? r : 0;
             continue;
           }
-          int qb[4];
+          f2 qb[2];  // RangeBN input: clamped quotient (rounded below)
           if (EK == EK_BNCODE || e.bn_mean) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              qb[u] = (int)quant_code_fast(v[u], e.bn_neg_min, e.bn_scale, bn_inv, e.bn_qmax);  // RangeBN input
+            qb[0] = qclamp2(v[0], bnp);
+            qb[1] = qclamp2(v[1], bnp);
           }
           if constexpr (EK == EK_BNCODE) {
-            k0[g] = cok ? (qb[0] | (qb[1] << 8) | (qb[2] << 16) | (qb[3] << 24)) : 0;
+            k0[g] = cok ? pack4(qb[0] + MAGIC_U8, qb[1] + MAGIC_U8) : 0;
             continue;
           } else {
             if (e.bn_mean) {
@@ -399,38 +409,35 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
               const float4 sq4 = *reinterpret_cast<const float4*>(s_f + 4 * BM + cl);
               const float4 wq4 = *reinterpret_cast<const float4*>(s_f + 5 * BM + cl);
               const float4 bq4 = *reinterpret_cast<const float4*>(s_f + 6 * BM + cl);
-              const float mn[4] = {mn4.x, mn4.y, mn4.z, mn4.w}, sq[4] = {sq4.x, sq4.y, sq4.z, sq4.w};
-              const float wq[4] = {wq4.x, wq4.y, wq4.z, wq4.w}, bq[4] = {bq4.x, bq4.y, bq4.z, bq4.w};
+              const f2 mn[2] = {{mn4.x, mn4.y}, {mn4.z, mn4.w}}, sq[2] = {{sq4.x, sq4.y}, {sq4.z, sq4.w}};
+              const f2 wq[2] = {{wq4.x, wq4.y}, {wq4.z, wq4.w}}, bq[2] = {{bq4.x, bq4.y}, {bq4.z, bq4.w}};
 #pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                float o = dequant((float)qb[u], e.bn_scale, e.bn_min) - mn[u];  // x - mean
-                o = o * sq[u];                                                   // * q(scale)
-                o = o * wq[u];                                                   // * q(weight)
-                v[u] = o + bq[u];                                                // + q(bias)
+              for (int h = 0; h < 2; ++h) {
+                f2 o = rint2(qb[h]) * bn_s2;  // dequant: q * s
+                o = o + bn_m2;                // + min
+                o = o - mn[h];                // x - mean
+                o = o * sq[h];                // * q(scale)
+                o = o * wq[h];                // * q(weight)
+                v[h] = o + bq[h];             // + q(bias)
               }
             }
-            float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
             if (has_res) {
               const float4 r4 = rcur[g];
-              o4.x = o4.x + r4.x; o4.y = o4.y + r4.y; o4.z = o4.z + r4.z; o4.w = o4.w + r4.w;
+              v[0] = v[0] + (f2){r4.x, r4.y};
+              v[1] = v[1] + (f2){r4.z, r4.w};
             }
             if (e.relu) {
-              o4.x = fmaxf(o4.x, 0.f); o4.y = fmaxf(o4.y, 0.f); o4.z = fmaxf(o4.z, 0.f); o4.w = fmaxf(o4.w, 0.f);
+              v[0].x = fmaxf(v[0].x, 0.f); v[0].y = fmaxf(v[0].y, 0.f);
+              v[1].x = fmaxf(v[1].x, 0.f); v[1].y = fmaxf(v[1].y, 0.f);
             }
             if (e.out_f32 && pok && cok) {
               const int64_t fi = e.f32_tiled ? ctile_index(pm[j], c, p.ct) : (int64_t)pm[j] * d.cout + c;
-              *reinterpret_cast<float4*>(e.out_f32 + fi) = o4;
+              *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
             }
-            if (e.out_code0 && cok) {
-              const float nm = e.code0_neg_min, s = e.code0_scale, q = e.code0_qmax;
-              k0[g] = code_byte(o4.x, nm, s, c0_inv, q) | (code_byte(o4.y, nm, s, c0_inv, q) << 8) |
-                      (code_byte(o4.z, nm, s, c0_inv, q) << 16) | (code_byte(o4.w, nm, s, c0_inv, q) << 24);
-            }
-            if (e.out_code1 && cok) {
-              const float nm = e.code1_neg_min, s = e.code1_scale, q = e.code1_qmax;
-              k1[g] = code_byte(o4.x, nm, s, c1_inv, q) | (code_byte(o4.y, nm, s, c1_inv, q) << 8) |
-                      (code_byte(o4.z, nm, s, c1_inv, q) << 16) | (code_byte(o4.w, nm, s, c1_inv, q) << 24);
-            }
+            if (e.out_code0 && cok)
+              k0[g] = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+            if (e.out_code1 && cok)
+              k1[g] = pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
           }
         }
         const int ch = cb + 16 * fh;

@@ -54,6 +54,52 @@ __device__ __forceinline__ float quant_code_fast(float x, float neg_min, float s
   return rintf(fminf(fmaxf(q, 0.0f), qmax));
 }
 
+// ---- packed-pair forms for the conv epilogues (v_pk_add/mul/fma_f32: two lanes' worth of
+// the same IEEE fp32 ops per VALU instruction, so results are bitwise those of the scalar
+// forms above)
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+struct QParams {  // one per-tensor quantizer: x -> code
+  float nm, s, inv, lim, qmax;  // -min, scale, RN(1/scale), 2^20*scale, 2^bits-1
+};
+
+__device__ __forceinline__ QParams make_qparams(float neg_min, float scale, float qmax) {
+  return {neg_min, scale, 1.0f / scale, 1048576.0f * scale, qmax};
+}
+
+// Clamped quotient clamp(RN((x + nm) / s), 0, qmax) of quant_code_fast for a pair, before
+// the final round.  The t clamp to +-2^20*s replaces quant_code_fast's |q0| < 2^20 select:
+// inside it the two are the same Markstein quotient, outside it both clamp to 0 / qmax.
+__device__ __forceinline__ f2 qclamp2(f2 x, const QParams& p) {
+  f2 t = x + p.nm;
+  t.x = __builtin_amdgcn_fmed3f(t.x, -p.lim, p.lim);
+  t.y = __builtin_amdgcn_fmed3f(t.y, -p.lim, p.lim);
+  const f2 inv = {p.inv, p.inv}, s = {p.s, p.s};
+  const f2 q0 = t * inv;
+  const f2 r = pfma(-q0, s, t);
+  f2 q = pfma(r, inv, q0);
+  q.x = __builtin_amdgcn_fmed3f(q.x, 0.0f, p.qmax);
+  q.y = __builtin_amdgcn_fmed3f(q.y, 0.0f, p.qmax);
+  return q;
+}
+
+__device__ __forceinline__ f2 rint2(f2 q) { return (f2){__builtin_rintf(q.x), __builtin_rintf(q.y)}; }
+
+// q in [0, 255] plus one of these lands in [2^23, 2^24) (ulp 1, even magic: RN-even ties
+// are those of rint), so the sum's low mantissa byte is rint(q) (U8) or rint(q) - 128 mod
+// 256 (S8, the int8 code' of the NHWC8 layout).
+constexpr float MAGIC_U8 = 12582912.0f;  // 1.5 * 2^23
+constexpr float MAGIC_S8 = 12582784.0f;  // 1.5 * 2^23 - 128
+
+// low bytes of four magic-shifted values -> one dword (byte u = value u)
+__device__ __forceinline__ int pack4(f2 a, f2 b) {
+  const unsigned p01 = __builtin_amdgcn_perm(__float_as_uint(a.y), __float_as_uint(a.x), 0x0c0c0400u);
+  const unsigned p23 = __builtin_amdgcn_perm(__float_as_uint(b.y), __float_as_uint(b.x), 0x0c0c0400u);
+  return (int)__builtin_amdgcn_perm(p23, p01, 0x05040100u);
+}
+
 __device__ __forceinline__ float dequant(float q, float scale, float min) {
   float v = q * scale;             // add_(-qmin).mul_(scale) :100
   return v + min;                  // add_(min_value)         :100
