@@ -1095,7 +1095,7 @@ static int pick_cfg(const Params& p) {
   }();
   auto ok = [&](int k) { return k >= 0 && k < NCFG && !((k == 0 || k == 6 || k == 9) && epi_kind(p.e) == EK_GEN); };
   if (ok(forced)) return forced;  // QNN_CONV_CFG: experiments override every caller
-  if (ok(p.d.tile - 1)) return p.d.tile - 1;
+  if (p.d.tile > 0) return ok(p.d.tile - 1) ? p.d.tile - 1 : -1;  // explicit: built, or an argument error
   int best = -1;
   double bc = 0;
   for (int k = 0; k < NCFG; ++k) {
@@ -1176,6 +1176,7 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   const int rc = conv_params(*desc, *epi, p);
   if (rc != QNN_OK) return rc;
   const int k = pick_cfg(p);
+  QNN_REQUIRE(k >= 0, "tile configuration not built for this epilogue kind");
   if (cfg) *cfg = k;
   if (bm) *bm = CFG[k].bm;
   if (bn) *bn = CFG[k].bn;
@@ -1214,7 +1215,9 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
                 "C-tile fp32 maps must be 16-byte aligned");
   }
   hipStream_t s = (hipStream_t)stream;
-  const int rc = launch_cfg(pick_cfg(p), x, wq, p, s);
+  const int k = pick_cfg(p);
+  QNN_REQUIRE(k >= 0, "tile configuration not built for this epilogue kind");
+  const int rc = launch_cfg(k, x, wq, p, s);
   if (rc != QNN_OK) return rc;
   QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
   return QNN_OK;

@@ -66,6 +66,12 @@ class ShardedInference:
         self.bounds = [shard_bounds(global_batch, self.world, r) for r in range(self.world)]
         self.max_shard = max(e - s for s, e in self.bounds)
         self._gather_bufs = None
+        planned = getattr(model, "N", None)  # a qnn.Engine runs exactly the batch it was built for
+        if planned is not None:
+            s, e = self.bounds[self.rank]
+            if e - s != planned:
+                raise ValueError(f"rank {self.rank}: shard of {e - s} samples but the engine is planned for "
+                                 f"{planned}; build each rank's Engine with its shard size")
 
     def local_slice(self):
         return self.bounds[self.rank]

@@ -70,7 +70,10 @@ class Engine:
     the model's device).  `engine.input` is a static input buffer; passing it (or
     nothing) avoids the copy.  graph=False runs the launches eagerly (debugging)."""
 
-    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True):
+    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None):
+        """tile=k forces tile configuration k on every contraction it is built for (the
+        others keep the cost model's choice); tile=None autotunes (or the cost model
+        when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile."""
         if model.training:
             raise RuntimeError("qnn.Engine: call model.eval() first (the engine is the eval forward)")
         self.model = model
@@ -83,6 +86,7 @@ class Engine:
         self.keep = []
         self.launch_names = []
         self.convs = []  # (op index, ConvDesc, Epilogue) of every contraction
+        self._bn_cache = {}  # RangeBN module -> BnParams: each module's range is read exactly once
         with torch.no_grad():
             if hasattr(model, "features") and hasattr(model, "fc"):
                 hw = input_hw or 224
@@ -101,8 +105,17 @@ class Engine:
             for (_i, d, _e), k in zip(self.convs, ks):
                 d.tile = k + 1
             self.tiles = [(k, None) for k in ks]
+        elif tile is not None:
+            self.tiles = []
+            for _i, d, e in self.convs:
+                d.tile = int(tile) + 1
+                if not self._plan_ok(d, e):
+                    d.tile = 0
+                self.tiles.append((self.plan(d, e)[0], None))
         elif autotune:
             self._autotune()
+        else:
+            self.tiles = [(self.plan(d, e)[0], None) for _i, d, e in self.convs]
         self.graph = None
         if graph:
             self._capture()
@@ -137,13 +150,34 @@ class Engine:
         return act.f32
 
     def _bn(self, bn):
+        b = self._bn_cache.get(bn)
+        if b is not None:
+            return b
         sq, wq, bq = bn._params(bn.running_var)
         mn, mx = bn.quantize_input._eval_range()
         b = _lib.BnParams(mean=bn.running_mean.data_ptr(), sq=sq.data_ptr(), wq=wq.data_ptr(), bq=bq.data_ptr(),
                           neg_min=-float(mn), min=float(mn), scale=float_scale(mn, mx, bn.num_bits),
                           qmax=_qmax(bn.num_bits))
         self.keep += [sq, wq, bq, b]
+        self._bn_cache[bn] = b
         return b
+
+    # ------------------------------------------------------------------ tile plans
+    @staticmethod
+    def plan(d, e):
+        """(configuration, bm, bn, blocks) qnn_qconv2d_fwd resolves for this launch."""
+        cfg, bm, bn_, nb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.call("qnn_conv_plan", ctypes.byref(d), ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(bm),
+                  ctypes.byref(bn_), ctypes.byref(nb))
+        return cfg.value, bm.value, bn_.value, nb.value
+
+    @staticmethod
+    def _plan_ok(d, e):
+        try:
+            Engine.plan(d, e)
+            return True
+        except _lib.QnnError:
+            return False
 
     # ------------------------------------------------------------------ ops
     def _add(self, name, fn):
@@ -461,6 +495,8 @@ class Engine:
                     ms = e0.elapsed_time(e1) / reps
                     if best is None or ms < best[1]:
                         best = (k, ms)
+                if best is None:
+                    raise RuntimeError("qnn.Engine: no tile configuration is built for a contraction of this plan")
                 d.tile = best[0] + 1
                 self.tiles.append(best)
             torch.cuda.synchronize(self.dev)
@@ -483,7 +519,12 @@ class Engine:
         torch.cuda.synchronize(self.dev)
 
     def __call__(self, x=None):
+        """Run one forward.  Returns the engine's static logits buffer [batch, classes]: the
+        next call overwrites it (clone() to keep a result)."""
         if x is not None and x.data_ptr() != self.input.data_ptr():
+            if tuple(x.shape) != tuple(self.input.shape):
+                raise ValueError(f"qnn.Engine: input shape {tuple(x.shape)} != the planned {tuple(self.input.shape)} "
+                                 "(the engine is built for one batch size)")
             self.input.copy_(x)
         if self.graph is not None:
             self.graph.replay()

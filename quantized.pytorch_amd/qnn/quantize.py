@@ -275,6 +275,9 @@ class _QLayerMixin:
 
     def _init_qcache(self):
         self._qpack = None
+        # qnn_conv_desc.tile of the int8 contraction: 0 = the library's cost model, k + 1 =
+        # configuration k (qnn_conv_plan); every configuration computes the identical result
+        self.qnn_tile = 0
 
     def _weight4(self):
         w = self.weight
@@ -284,7 +287,13 @@ class _QLayerMixin:
         w = self.weight
         bias = self.bias
         freeze = bool(self.freeze_param_dyn_range)
-        key = (w.data_ptr(), w._version, None if bias is None else (bias.data_ptr(), bias._version), freeze,
+        frozen = None
+        if freeze:  # the frozen range buffers feed the quantizers: their versions key the pack too
+            frozen = tuple((t.data_ptr(), t._version) for t in (self.weight_min, self.weight_max,
+                                                                  getattr(self, "bias_min", None),
+                                                                  getattr(self, "bias_max", None))
+                           if torch.is_tensor(t))
+        key = (w.data_ptr(), w._version, None if bias is None else (bias.data_ptr(), bias._version), freeze, frozen,
                self.num_bits_weight, self.bias_quant, depthwise, s2d, w.device)
         pk = self._qpack
         if pk is not None and pk.key == key:
@@ -334,7 +343,14 @@ class _QLayerMixin:
         if bias is not None:
             b = bias.detach().contiguous()
             rng = torch.empty(2, dtype=torch.float32, device=dev)
-            if self.bias_quant:
+            if self.bias_quant and freeze:
+                # frozen: quantize(bias, min_value=self.bias_min, max_value=self.bias_max) (quantize.py:336-338)
+                pk.qbias = torch.empty_like(b)
+                bmin = self.bias_min.detach().reshape(1).float().contiguous()
+                bmax = self.bias_max.detach().reshape(1).float().contiguous()
+                _lib.call("qnn_fake_quant_rows_f32", _lib.ptr(b), _lib.ptr(pk.qbias), 1, b.numel(), _lib.ptr(bmin),
+                          _lib.ptr(bmax), qmax, st)
+            elif self.bias_quant:
                 pk.qbias = torch.empty_like(b)
                 _lib.call("qnn_fake_quant_vec_f32", _lib.ptr(b), _lib.ptr(pk.qbias), b.numel(), qmax, 0,
                           _lib.ptr(rng), st)
@@ -426,6 +442,7 @@ class _QLayerMixin:
                       qmax, st)
         d.zero_off = nbytes
         d.kmask = None if pk.kmask is None else pk.kmask.data_ptr()
+        d.tile = int(self.qnn_tile)
         g = self._geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev)
         sxsw, sxbw, table = self._epilogue(pk, g, (H, W), s32, b_x, kh, kw)
         y = torch.empty((N, cout, Ho, Wo), dtype=torch.float32, device=dev)

@@ -238,8 +238,8 @@ def test_model_layers_teacher_forced(gpu, name):
     for h in hooks:
         h.remove()
     assert len(seen) > 20
-    worst = 0.0
-    for m, xin, yout in seen:
+    worst, worst_flip, flips = 0.0, 0.0, []
+    for i, (m, xin, yout) in enumerate(seen):
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         rng = O.measure_range(sd, "quantize_input.")
         if isinstance(m, RangeBN):
@@ -251,7 +251,20 @@ def test_model_layers_teacher_forced(gpu, name):
         else:
             ref = O.qconv2d(xin, sd["weight"], sd.get("bias"), m.stride, m.padding, 1, m.groups, rng)
         worst = max(worst, _close(yout, ref) / ref.abs().max().item())
-    print(f"{name}: {len(seen)} layers, worst max|dy|/max|y| = {worst:.2e}")
+        # fraction of the consumer's activation codes that the fp32 epilogue
+        # rounding flips (the conv output feeds the next RangeBN's quantizer directly)
+        if i + 1 < len(seen) and isinstance(seen[i + 1][0], RangeBN) and torch.equal(seen[i + 1][1], yout):
+            bsd = {k: v.detach().cpu() for k, v in seen[i + 1][0].state_dict().items()}
+            lo, hi = O.measure_range(bsd, "quantize_input.")
+            qg = O.quantize_codes_np(yout.numpy(), lo, hi)
+            qr = O.quantize_codes_np(ref.numpy(), lo, hi)
+            frac = float((qg != qr).mean())
+            flips.append(frac)
+            worst_flip = max(worst_flip, frac)
+    print(f"{name}: {len(seen)} layers, worst max|dy|/max|y| = {worst:.2e}; flipped consumer codes per layer: "
+          f"max {worst_flip:.2e}, mean {np.mean(flips) if flips else 0.0:.2e} over {len(flips)} conv->RangeBN pairs")
+    assert flips, "no conv -> RangeBN pair found"
+    assert worst_flip <= 1e-3, f"flipped-code fraction {worst_flip:.2e} > 1e-3"
 
 
 @pytest.mark.parametrize("name", MODELS)
