@@ -192,6 +192,13 @@ int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc
  * QNN_CONV_CFG=<id> in the environment forces a configuration. Any out pointer may be NULL. */
 int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn, int* nblk);
 
+/* Number of tile configurations (valid qnn_conv_desc.tile values are 1 .. count).  Those with
+ * ids >= 12 are the halo-band kernels for kh x kw > 1: the block's input rows are read into
+ * LDS once per K chunk and every tap reads them at a shifted LDS address (no im2col
+ * re-reads from L2).  An explicit tile that is not built for the layer / epilogue kind is an
+ * argument error. */
+int qnn_conv_tile_count(void);
+
 /* Depthwise (groups == cin == cout) eval forward: fake-quantize-on-load of x
  * (QuantMeasure range) times the dequantized weights w_hat [c][kh*kw] plus the
  * fake-quantized bias, fp32.  NCHW in, NCHW out. */

@@ -985,9 +985,325 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(2))) void
 #endif
 }
 
+// ---------------------------------------------------------------- halo-band main loop
+// For kh x kw > 1 the implicit im2col of qconv_kernel pulls every input byte through
+// L2 -> LDS once per tap (9x for 3x3, 16x for the space-to-depth 7x7 stem): on CDNA4
+// the per-CU L2 -> LDS rate (~30 B/clk), not the MFMA pipe, bounds those layers.  Here
+// a block loads the BAND of input rows its BN output pixels read -- once per K chunk --
+// into LDS, and every tap's B fragment is an LDS read at a tap-shifted band address.
+// Only the weights stream per K stage (through the D-slot LDS ring, as before).
+//
+// K order: chunk c of Cp (16 << LW bytes of channels per band pixel, LW = 2 for
+// Cp >= 64), then taps (row-major), then the chunk's 16-byte slots -- which is the
+// tap-major packed weight row read at column t*Cp + 64c (LW = 2) or 64s (one chunk).
+// A 64-byte stage is one tap (LW 2), two taps (LW 1, Cp 32) or four (LW 0, Cp 16).
+//
+// Band layout: pixel q of the band (padded input rows [R0, R1), stride-2 convs with
+// each row's even columns first) holds its chunk at q * (16 << LW), the 16-byte slots
+// XOR-swizzled by q's bits [4-LW, 4) so that the 32 consecutive pixels of a 32x32x32
+// B fragment hit 16 distinct bank slots per ds_read_b128 lane group.  The swizzle is
+// applied on the DMA source side (LDS-DMA destinations are lane-linear).
+struct Band {
+  int nc, ns, kt;                   // K chunks, 64-B stages per chunk, stages in all
+  int s2, we;                       // stride 2: deinterleaved columns, even count (wp + 1) / 2
+  uint32_t wp_magic;                // ceil(2^32 / wp): q / wp == umulhi(q, wp_magic)
+  int nbw;                          // band DMA pieces (1 KiB) per wave per chunk
+  int band_off, band_bytes, nbuf;   // LDS: band buffers (2 when nc > 1)
+  int zero_off, mask_off;           // LDS: 64 zero bytes (padded taps), K mask (MASKED)
+};
+
+// vmcnt(n) for a run-time n (uniform): the exact count or a smaller one (waits longer)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  if (n >= 24) wait_vmcnt<24>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else switch (n) {
+      case 15: wait_vmcnt<15>(); break;
+      case 14: wait_vmcnt<14>(); break;
+      case 13: wait_vmcnt<13>(); break;
+      case 12: wait_vmcnt<12>(); break;
+      case 11: wait_vmcnt<11>(); break;
+      case 10: wait_vmcnt<10>(); break;
+      case 9: wait_vmcnt<9>(); break;
+      case 8: wait_vmcnt<8>(); break;
+      case 7: wait_vmcnt<7>(); break;
+      case 6: wait_vmcnt<6>(); break;
+      case 5: wait_vmcnt<5>(); break;
+      case 4: wait_vmcnt<4>(); break;
+      case 3: wait_vmcnt<3>(); break;
+      case 2: wait_vmcnt<2>(); break;
+      case 1: wait_vmcnt<1>(); break;
+      default: wait_vmcnt<0>(); break;
+    }
+}
+
+template <int LW>
+__device__ __forceinline__ int band_slot_xor(int q) {  // swizzle of band pixel q's 16-byte slots
+  if constexpr (LW == 0) return 0;
+  else return (q >> (4 - LW)) & ((1 << LW) - 1);
+}
+
+template <class C, int EK, int LW, bool MASKED>
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_band_kernel(
+    const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Band bd) {
+  constexpr int BM = C::BM, BN = C::BN, W = C::W, TM = C::TM, TN = C::TN, D = C::NS, NA = C::NA;
+  constexpr int PS = 16 << LW;     // band pixel bytes (one K chunk)
+  constexpr int STAGE_A = BM * 64;
+  static_assert(C::BK == 64, "band kernel: 64-byte weight stages");
+  static_assert(!MASKED || LW == 0, "masked (space-to-depth) stems have 16-channel band pixels");
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nbx = (p.M + BN - 1) / BN;
+  const int nblk = nbx * nby;
+  int t;
+  {
+    const int bb = blockIdx.x, xcd = bb & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bb >> 3);
+  }
+  const int m0 = (t / nby) * BN;
+  const int c0 = (t % nby) * BM;
+  const int HoWo = d.ho * d.wo;
+  auto grow = [&](int m) {  // padded input row (over the whole batch) of output pixel m's tap row 0
+    const int n = m / HoWo, r = m - n * HoWo, ho = r / d.wo;
+    return n * d.hp + ho * d.sh;
+  };
+  const int R0 = __builtin_amdgcn_readfirstlane(grow(m0));
+  const int mlast = (m0 + BN < p.M ? m0 + BN : p.M) - 1;
+  const int NBP = __builtin_amdgcn_readfirstlane((grow(mlast) + d.kh - R0) * d.wp);
+
+  if (tid < 4) *reinterpret_cast<v4i*>(smem + bd.zero_off + 16 * tid) = (v4i){0, 0, 0, 0};
+  if constexpr (MASKED) {
+    for (int i = tid; i < d.kpad / 16; i += C::NT)
+      *reinterpret_cast<v4i*>(smem + bd.mask_off + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
+  }
+  __syncthreads();  // before any LDS-DMA is in flight (a barrier then would drain it)
+
+  // ---- per-lane state: this lane's pixel of each column tile j as a band pixel (tap 0,0)
+  const int frow = lane & 31, fh = lane >> 5;
+  int pb[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int m = m0 + wn * 32 * TN + j * 32 + frow;
+    m = m < p.M ? m : p.M - 1;
+    const int n = m / HoWo, r = m - n * HoWo, ho = r / d.wo, wo = r - ho * d.wo;
+    pb[j] = (n * d.hp + ho * d.sh - R0) * d.wp + wo;  // input column wo*sw: wo itself (s2: even half)
+  }
+  const int8_t* wblk = w + (int64_t)c0 * d.kpad;
+  uint32_t aoff[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int row = 16 * (wave + W * j) + lane / 4;
+    const int crow = (c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0);
+    aoff[j] = (uint32_t)(crow * d.kpad + (swz<64>(row, lane % 4) - row * 64));
+  }
+  int pcls[TN];
+  pixel_classes<C>(p, m0, wn, lane, pcls);
+  if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
+
+  // ---- DMA issue
+  auto issue_band = [&](int c, int bi) {
+    int8_t* dst = smem + bd.band_off + bi * bd.band_bytes;
+    for (int k = 0; k < bd.nbw; ++k) {
+      const int piece = wave + W * k;
+      const int byte = piece * 1024 + 16 * lane;
+      int q = byte >> (4 + LW);
+      q = q < NBP ? q : NBP - 1;
+      const int u = ((byte >> 4) & ((1 << LW) - 1)) ^ band_slot_xor<LW>(q);
+      const int r = (int)__umulhi((uint32_t)q, bd.wp_magic);
+      const int ci = q - r * d.wp;
+      const int col = bd.s2 ? (ci < bd.we ? 2 * ci : 2 * (ci - bd.we) + 1) : ci;
+      uint32_t off = (uint32_t)(((R0 + r) * d.wp + col) * d.cp + c * PS + 16 * u);
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(dst + piece * 1024), 16, 0, 0);
+    }
+  };
+  auto koff = [&](int c, int s) -> uint32_t {  // packed weight column of stage (c, s)
+    if constexpr (LW == 2) return (uint32_t)(s * d.cp + 64 * c);
+    else return (uint32_t)(64 * s);
+  };
+  auto issue_w = [&](int c, int s, int slot) {
+    if (QNN_ABLATE == 1) return;
+    const uint32_t ko = koff(c, s);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      uint32_t off = aoff[j] + ko;
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(smem + slot * STAGE_A + (wave + W * j) * 1024),
+                                       16, 0, 0);
+    }
+  };
+  // band offset of tap t (uniform)
+  auto tap_delta = [&](int tt) {
+    const int tr = (tt * p.kw_magic) >> 16, tc = tt - tr * d.kw;
+    return tr * d.wp + (bd.s2 ? (tc & 1) * bd.we + (tc >> 1) : tc);
+  };
+
+  v16i acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v16i){0};
+  int sumq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) sumq[j] = 0;
+  int offa[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) offa[ks] = (wm * 32 * TM + frow) * 64 + (swz<64>(frow, 2 * ks + fh) - frow * 64);
+
+  // one 64-byte stage: 2 k-steps of 32x32x32; B fragments read from the band at tap-shifted
+  // addresses (padded taps of LW < 2 read the zero bytes)
+  auto compute = [&](auto slotc, int bi, int s) {
+    constexpr int AO = decltype(slotc)::value * STAGE_A;
+    const int bbase = bd.band_off + bi * bd.band_bytes;
+    v4i fa[2][TM], fb[2][TN];
+    auto load = [&](int ks, int sl) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[sl][i] = *reinterpret_cast<const v4i*>(smem + AO + offa[ks] + i * 32 * 64);
+      int tt, u;
+      if constexpr (LW == 2) tt = s, u = 2 * ks + fh;
+      else if constexpr (LW == 1) tt = 2 * s + ks, u = fh;
+      else tt = 4 * s + 2 * ks + fh, u = 0;
+      int dl;
+      if constexpr (LW == 0) {
+        const int t0 = 4 * s + 2 * ks;
+        const int d0 = tap_delta(t0), d1 = tap_delta(t0 + 1);
+        dl = fh ? d1 : d0;
+      } else {
+        dl = tap_delta(tt);
+      }
+      const bool pad = tt >= p.taps;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int q = pb[j] + dl;
+        int addr = bbase + q * PS + ((u ^ band_slot_xor<LW>(q)) << 4);
+        if (LW < 2) addr = pad ? bd.zero_off : addr;
+        fb[sl][j] = *reinterpret_cast<const v4i*>(smem + addr);
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < 2) load(ks + 1, cur ^ 1);
+      v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
+      if constexpr (MASKED) ones = *reinterpret_cast<const v4i*>(smem + bd.mask_off + s * 64 + 16 * (2 * ks + fh));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int sm = __builtin_amdgcn_sdot4(fb[cur][j].x, ones.x, sumq[j], false);
+        sm = __builtin_amdgcn_sdot4(fb[cur][j].y, ones.y, sm, false);
+        sm = __builtin_amdgcn_sdot4(fb[cur][j].z, ones.z, sm, false);
+        sumq[j] = __builtin_amdgcn_sdot4(fb[cur][j].w, ones.w, sm, false);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (QNN_ABLATE == 2) {
+            asm volatile("" ::"v"(fa[cur][i]), "v"(fb[cur][j]));
+            acc[i][j][0] += fa[cur][i].x;
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+  };
+
+  // ---- prologue: band chunk 0, weight stages 0 .. D-2 (clamped: counts stay uniform)
+  const int KT = bd.kt;
+  issue_band(0, 0);
+  {
+    int c = 0, s = 0;
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) {
+      issue_w(c, s, k);
+      if (k + 1 < KT) {
+        if (++s == bd.ns) s = 0, ++c;
+      }
+    }
+  }
+  // stage k = (c, s) lives in weight slot k % D and band buffer c & 1.  Before the barrier
+  // of stage k each wave waits for its own DMA of stage k (issued D-1 stages earlier; the
+  // band chunk it reads is older still); the younger DMAs may stay in flight: D-2 weight
+  // stages, plus the next band chunk when it was issued within them.
+  int c = 0, s = 0;    // current stage
+  int ca = 0, sa = 0;  // the newest issued weight stage: D-2 (clamped to the last one)
+  for (int k = 0; k < D - 2 && k + 1 < KT; ++k)
+    if (++sa == bd.ns) sa = 0, ++ca;
+  auto step = [&](auto slotc) {
+    constexpr int SL = decltype(slotc)::value;
+    const bool band_young = s >= 1 && s <= D - 2 && c + 1 < bd.nc;
+    wait_vmcnt_rt((D - 2) * NA + (band_young ? bd.nbw : 0));
+    __builtin_amdgcn_s_barrier();
+    if (s == 0 && c + 1 < bd.nc) issue_band(c + 1, (c + 1) & 1);
+    // advance the issue-ahead stage (clamped at the last stage) and refill the freed slot
+    if (ca * bd.ns + sa + 1 < KT) {
+      if (++sa == bd.ns) sa = 0, ++ca;
+    }
+    issue_w(ca, sa, (SL + D - 1) % D);
+    compute(slotc, c & 1, s);
+    if (++s == bd.ns) s = 0, ++c;
+  };
+  for (int k = 0; k < KT; k += D) {
+    step(std::integral_constant<int, 0>{});
+    if (k + 1 < KT) step(std::integral_constant<int, 1>{});
+    if (k + 2 < KT) step(std::integral_constant<int, 2>{});
+    if constexpr (D == 4)
+      if (k + 3 < KT) step(std::integral_constant<int, 3>{});
+  }
+  wait_vmcnt<0>();  // the clamped tail DMAs still write LDS
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
+  __syncthreads();  // main-loop LDS is reused by the epilogue
+  if (QNN_ABLATE == 3) {
+    int z = sumq[0];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z ^= acc[i][j][r];
+    if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;
+    return;
+  }
+  if (!p.epi_early) {
+    stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+  epilogue<C, EK>(p, acc, sumq, pcls, smem, m0, c0, wm, wn, lane, tid, wave);
+}
+
 template <class C>
 static int main_lds_bytes(int tapm, bool masked) {
   return C::NS * C::STAGE + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
+}
+
+constexpr int LDS_MAX = 160 * 1024;
+
+// LDS of a launch: main loop (lds_main bytes at 0), epilogue data (early: beside the main
+// loop's LDS, DMA'd at kernel start; late: at 0 once the main loop is done), NCHW transpose
+// scratch (after the loop).  Returns the dynamic LDS bytes, or -1 if over 160 KiB.
+template <class C>
+static int plan_epi_lds(int lds_main, Params& q) {
+  lds_main = (lds_main + 15) & ~15;
+  const int k = epi_kind(q.e);
+  const int epi = 4 * (7 + q.e.nclass) * C::BM + (k == EK_LUT ? 256 * C::BM : 0);
+  const int scr = k == EK_NCHW ? 4096 * C::W : 0;
+  int lds;
+  if (lds_main + epi <= LDS_MAX / C::BPC && scr <= lds_main) {
+    q.epi_early = 1, q.epi_off = lds_main, q.scr_off = 0;
+    lds = lds_main + epi;
+  } else {
+    q.epi_early = 0, q.epi_off = 0, q.scr_off = (epi + 15) & ~15;
+    lds = q.scr_off + scr > lds_main ? q.scr_off + scr : lds_main;
+  }
+  return lds > LDS_MAX ? -1 : lds;
 }
 
 template <class C, int PP, int EK, int TAPM, bool MASKED>
@@ -999,26 +1315,90 @@ static int launch_kernel(const int8_t* x, const int8_t* w, const Params& p, hipS
   static const hipError_t attr =  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
-  // LDS: main-loop ring (+ tap table / K mask), epilogue data (early: beside the ring,
-  // late: at 0 once the ring is free), NCHW transpose scratch (after the loop)
-  constexpr int LDS_MAX = 160 * 1024;
-  const int lds_main = (main_lds_bytes<C>(TAPM, MASKED) + 15) & ~15;
-  const int k = epi_kind(p.e);
-  const int epi = 4 * (7 + p.e.nclass) * C::BM + (k == EK_LUT ? 256 * C::BM : 0);
-  const int scr = k == EK_NCHW ? 4096 * C::W : 0;
   Params q = p;
-  int lds;
-  if (lds_main + epi <= LDS_MAX / C::BPC && scr <= lds_main) {
-    q.epi_early = 1, q.epi_off = lds_main, q.scr_off = 0;
-    lds = lds_main + epi;
-  } else {
-    q.epi_early = 0, q.epi_off = 0, q.scr_off = (epi + 15) & ~15;
-    lds = q.scr_off + scr > lds_main ? q.scr_off + scr : lds_main;
-  }
-  if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+  const int lds = plan_epi_lds<C>(main_lds_bytes<C>(TAPM, MASKED), q);
+  if (lds < 0) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
   const int nblk = (int)(cdiv(p.M, C::BN) * cdiv(p.d.cout, C::BM));
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q);
   return QNN_OK;
+}
+
+// ---- halo-band kernel: geometry and LDS of a layer for a (BM, BN, waves, ring depth)
+static int band_lw(const qnn_conv_desc& d) { return d.cp >= 64 ? 2 : (d.cp == 32 ? 1 : 0); }
+
+// Fills the K schedule and band sizing; returns the main-loop LDS bytes, or -1 when the
+// layer is not a band layer (1x1, unsupported stride) or the band does not fit.
+static int band_geometry(const Params& p, int BM, int BN, int nwaves, int D, int bpc, Band& b) {
+  const qnn_conv_desc& d = p.d;
+  if (p.taps <= 1 || d.sh != d.sw || (d.sh != 1 && d.sh != 2)) return -1;
+  const int lw = band_lw(d), W = 1 << lw, tps = 4 / W;
+  if (d.kmask && lw != 0) return -1;
+  const int taps_pad = (p.taps + tps - 1) / tps * tps;
+  b.nc = lw == 2 ? d.cp / 64 : 1;
+  b.ns = taps_pad / tps;
+  b.kt = b.nc * b.ns;
+  if (b.nc > 1 && b.ns < D - 1) return -1;
+  if ((lw < 2 ? b.ns * 64 : p.taps * d.cp) > d.kpad) return -1;
+  b.s2 = d.sh == 2;
+  b.we = (d.wp + 1) / 2;
+  b.wp_magic = (uint32_t)((0x100000000ULL + (uint64_t)d.wp - 1) / (uint64_t)d.wp);
+  // largest band over the tiles: BN consecutive output pixels span at most RO + 1 output
+  // rows and ceil-many image crossings, each adding hp - ho*sh padded rows
+  const int RO = (BN + d.wo - 2) / d.wo;
+  const int cross = (d.ho - 1 + RO) / d.ho;
+  const int nrows = RO * d.sh + cross * (d.hp - d.ho * d.sh) + d.kh;
+  const int64_t nbp = (int64_t)nrows * d.wp;
+  const int64_t pieces = cdiv(nbp * (16 << lw), 1024);
+  b.nbw = (int)cdiv(pieces, nwaves);
+  b.band_bytes = b.nbw * nwaves * 1024;
+  b.nbuf = b.nc > 1 ? 2 : 1;
+  b.band_off = D * BM * 64;
+  b.zero_off = b.band_off + b.nbuf * b.band_bytes;
+  b.mask_off = b.zero_off + 64;
+  const int lds = b.mask_off + (d.kmask ? d.kpad : 0);
+  if (b.nbw > 16 || lds > LDS_MAX / bpc) return -1;
+  return lds;
+}
+
+template <class C, int EK, int LW, bool MASKED>
+static int launch_band(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  auto kern = qconv_band_kernel<C, EK, LW, MASKED>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  Band b;
+  const int main = band_geometry(p, C::BM, C::BN, C::W, C::NS, C::BPC, b);
+  if (main < 0) return arg_error("band tile does not fit this layer");
+  Params q = p;
+  const int lds = plan_epi_lds<C>(main, q);
+  if (lds < 0) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+  const int nblk = (int)(cdiv(p.M, C::BN) * cdiv(p.d.cout, C::BM));
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q, b);
+  return QNN_OK;
+}
+
+template <class C, int EK>
+static int launch_band_lw(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  const int lw = band_lw(p.d);
+  if (lw == 2) return launch_band<C, EK, 2, false>(x, w, p, s);
+  if constexpr (C::BM == 64) {  // few-channel layers (stems, CIFAR) have few output channels
+    if (p.d.kmask) return launch_band<C, EK, 0, true>(x, w, p, s);
+    if (lw == 1) return launch_band<C, EK, 1, false>(x, w, p, s);
+    return launch_band<C, EK, 0, false>(x, w, p, s);
+  }
+  return arg_error("band tile not built for this channel count");
+}
+
+template <class C>
+static int launch_band_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  switch (epi_kind(p.e)) {
+    case EK_NCHW: return launch_band_lw<C, EK_NCHW>(x, w, p, s);
+    case EK_LUT: return launch_band_lw<C, EK_LUT>(x, w, p, s);
+    case EK_BNCODE: return launch_band_lw<C, EK_BNCODE>(x, w, p, s);
+    default:
+      if constexpr (C::TM * C::TN >= 8) return arg_error("general fused epilogue not built for this tile");
+      else return launch_band_lw<C, EK_GEN>(x, w, p, s);
+  }
 }
 
 template <class C, int PP, int EK>
@@ -1064,17 +1444,45 @@ using C7 = Cfg<2, 4, 2, 2, 64, 4>;  // 128 x 256 ping-pong, waves 64 x 64, 2 k-s
 using C8 = Cfg<4, 2, 2, 2, 64, 4>;  // 256 x 128 ping-pong
 using C10 = Cfg<1, 4, 2, 2, 64, 3, 2>;  // 64 x 256, 3-slot ring: 2 blocks/CU with a stem's K mask
 using C11 = Cfg<1, 4, 2, 1, 64, 3, 4>;  // 64 x 128, 3-slot ring: 4 blocks/CU (short-K, epilogue-bound layers)
-constexpr int NCFG = 12;  // 9: C6 with 2 k-steps per phase
+// halo-band configurations (qconv_band_kernel; kh x kw > 1 only), 3-slot weight ring
+//   12  256 x 256   8 waves (128 x 64)   1 block/CU
+//   13  128 x 256   8 waves (64 x 64)    1
+//   14  256 x 128   8 waves (64 x 64)    1
+//   15   64 x 256   4 waves (64 x 64)    2   (also stems and 16/32-channel inputs)
+//   16  128 x 128   4 waves (64 x 64)    2
+//   17   64 x 128   2 waves (64 x 64)    4   (also stems and 16/32-channel inputs)
+using B12 = Cfg<2, 4, 4, 2, 64, 3, 1>;
+using B13 = Cfg<2, 4, 2, 2, 64, 3, 1>;
+using B14 = Cfg<4, 2, 2, 2, 64, 3, 1>;
+using B15 = Cfg<1, 4, 2, 2, 64, 3, 2>;
+using B16 = Cfg<2, 2, 2, 2, 64, 3, 2>;
+using B17 = Cfg<1, 2, 2, 2, 64, 3, 4>;
+constexpr int NCFG = 18;  // 9: C6 with 2 k-steps per phase
 struct CfgInfo {
-  int bm, bn, per_cu;
+  int bm, bn, per_cu, waves;
   float rate;  // relative MFMA throughput per CU (bytes moved per op, measured)
+  bool band;
 };
 static const CfgInfo CFG[NCFG] = {
-    {256, 256, 1, 1.00f}, {128, 256, 1, 0.85f}, {256, 128, 1, 0.85f},
-    {64, 256, 2, 0.70f},  {128, 128, 2, 0.70f}, {64, 128, 2, 0.50f},
-    {256, 256, 1, 1.20f}, {128, 256, 1, 0.95f}, {256, 128, 1, 0.95f}, {256, 256, 1, 1.15f},
-    {64, 256, 2, 0.70f},  {64, 128, 4, 0.45f},
+    {256, 256, 1, 8, 1.00f, false}, {128, 256, 1, 8, 0.85f, false}, {256, 128, 1, 8, 0.85f, false},
+    {64, 256, 2, 4, 0.70f, false},  {128, 128, 2, 4, 0.70f, false}, {64, 128, 2, 2, 0.50f, false},
+    {256, 256, 1, 8, 1.20f, false}, {128, 256, 1, 8, 0.95f, false}, {256, 128, 1, 8, 0.95f, false},
+    {256, 256, 1, 8, 1.15f, false}, {64, 256, 2, 4, 0.70f, false},  {64, 128, 4, 4, 0.45f, false},
+    {256, 256, 1, 8, 1.60f, true},  {128, 256, 1, 8, 1.40f, true},  {256, 128, 1, 8, 1.40f, true},
+    {64, 256, 2, 4, 1.20f, true},   {128, 128, 2, 4, 1.10f, true},  {64, 128, 4, 2, 0.90f, true},
 };
+
+// Whether configuration k is built for (and fits) this layer and epilogue kind
+static bool cfg_ok(int k, const Params& p) {
+  if (k < 0 || k >= NCFG) return false;
+  const int ek = epi_kind(p.e);
+  const CfgInfo& c = CFG[k];
+  if (ek == EK_GEN && (k == 0 || k == 6 || k == 9 || k == 12)) return false;  // 256x256 + general chain
+  if (!c.band) return true;
+  if (band_lw(p.d) < 2 && c.bm != 64) return false;
+  Band b;
+  return band_geometry(p, c.bm, c.bn, c.waves, 3, c.per_cu, b) >= 0;
+}
 
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
@@ -1093,7 +1501,7 @@ static int pick_cfg(const Params& p) {
     const char* v = getenv("QNN_CONV_CFG");
     return v ? atoi(v) : -1;
   }();
-  auto ok = [&](int k) { return k >= 0 && k < NCFG && !((k == 0 || k == 6 || k == 9) && epi_kind(p.e) == EK_GEN); };
+  auto ok = [&](int k) { return cfg_ok(k, p); };
   if (ok(forced)) return forced;  // QNN_CONV_CFG: experiments override every caller
   if (p.d.tile > 0) return ok(p.d.tile - 1) ? p.d.tile - 1 : -1;  // explicit: built, or an argument error
   int best = -1;
@@ -1119,7 +1527,13 @@ static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, 
     case 8: return launch_ek<C8, 2>(x, w, p, s);
     case 9: return launch_ek<C6, 2>(x, w, p, s);
     case 10: return launch_ek<C10>(x, w, p, s);
-    default: return launch_ek<C11>(x, w, p, s);
+    case 11: return launch_ek<C11>(x, w, p, s);
+    case 12: return launch_band_ek<B12>(x, w, p, s);
+    case 13: return launch_band_ek<B13>(x, w, p, s);
+    case 14: return launch_band_ek<B14>(x, w, p, s);
+    case 15: return launch_band_ek<B15>(x, w, p, s);
+    case 16: return launch_band_ek<B16>(x, w, p, s);
+    default: return launch_band_ek<B17>(x, w, p, s);
   }
 }
 
@@ -1168,6 +1582,8 @@ static int conv_params(const qnn_conv_desc& d, const qnn_epilogue& e, Params& p)
   p.stagger = stagger;
   return QNN_OK;
 }
+
+extern "C" int qnn_conv_tile_count(void) { return NCFG; }
 
 extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn,
                              int* nblk) {

@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
 ABI_VERSION = 5
-CONV_TILES = 12  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1)
+CONV_TILES = 18  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -115,6 +115,11 @@ def load(path=None):
     v = lib.qnn_abi_version()
     if v != ABI_VERSION:
         raise QnnLibraryError(f"qnn: ABI version mismatch (library {v}, bindings {ABI_VERSION})")
+    lib.qnn_conv_tile_count.restype = c_int
+    lib.qnn_conv_tile_count.argtypes = []
+    if lib.qnn_conv_tile_count() != CONV_TILES:
+        raise QnnLibraryError(f"qnn: library has {lib.qnn_conv_tile_count()} conv tile configurations, "
+                              f"bindings expect {CONV_TILES}")
     _lib = lib
     return lib
 

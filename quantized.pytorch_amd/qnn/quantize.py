@@ -278,6 +278,7 @@ class _QLayerMixin:
         # qnn_conv_desc.tile of the int8 contraction: 0 = the library's cost model, k + 1 =
         # configuration k (qnn_conv_plan); every configuration computes the identical result
         self.qnn_tile = 0
+        self.qnn_keep_input = False
 
     def _weight4(self):
         w = self.weight
@@ -455,6 +456,7 @@ class _QLayerMixin:
         e.out_f32 = y.data_ptr()
         _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
         self._last_conv = (d, e)  # launch descriptors, for profiling tools (qnn_conv_plan)
+        self._last_xq = xq if self.qnn_keep_input else None  # the codes, for tools that re-issue the launch
         return y
 
 
