@@ -1592,7 +1592,7 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   const int rc = conv_params(*desc, *epi, p);
   if (rc != QNN_OK) return rc;
   const int k = pick_cfg(p);
-  QNN_REQUIRE(k >= 0, "tile configuration not built for this epilogue kind");
+  QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   if (bm) *bm = CFG[k].bm;
   if (bn) *bn = CFG[k].bn;
@@ -1632,7 +1632,7 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
   }
   hipStream_t s = (hipStream_t)stream;
   const int k = pick_cfg(p);
-  QNN_REQUIRE(k >= 0, "tile configuration not built for this epilogue kind");
+  QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   const int rc = launch_cfg(k, x, wq, p, s);
   if (rc != QNN_OK) return rc;
   QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
