@@ -34,13 +34,9 @@
 
 #include <type_traits>
 
-#include "qnn_internal.h"
+#include "qconv_common.h"
 
 namespace qnn {
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 #ifndef QNN_ABLATE
 #define QNN_ABLATE 0  // diagnostic builds only (make ablate): 1 no loads, 2 no MFMA, 3 no epilogue
@@ -71,27 +67,6 @@ __device__ unsigned long long qnn_dbg_epi[1 << 18];  // [block][wave][4]: stagin
 #define QNN_TSV(v) ((void)0)
 #endif
 
-constexpr int MAX_TAPS = 64;
-constexpr int MAX_CLASSES = 32;
-constexpr int MAX_MASK = 1024;
-constexpr int KPAD_ALIGN = 128;  // packed weight rows are multiples of 128 bytes (any BK divides)
-constexpr int NUM_CU = 256;
-
-enum { TAP_ONE = 0, TAP_TWO = 1, TAP_LDS = 2 };
-
-struct Params {
-  qnn_conv_desc d;
-  qnn_epilogue e;
-  int M;         // n*ho*wo
-  int taps;      // kh*kw
-  int lgcpt;     // log2(cp/16): 16-byte chunks per tap
-  int kw_magic;  // ceil(2^16 / kw): t / kw == (t * kw_magic) >> 16 for t < 64
-  int ct;        // C-tile columns, ceil(cout / 32)
-  int stagger;   // 8-wave blocks: waves 4-7 refill after computing (QNN_CONV_STAGGER=0 disables)
-  int epi_off;   // LDS byte offset of the epilogue data (stage_epi)
-  int epi_early; // 1: staged by LDS-DMA at kernel start (lands during the main loop), 0: after it
-  int scr_off;   // LDS byte offset of the NCHW transpose scratch (used after the main loop)
-};
 
 // Tile configuration: WGM x WGN waves, each (32*TM) x (32*TN) (cout x pixels), K stage
 // BK bytes, NS-slot LDS ring.
@@ -122,11 +97,6 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   else return row * BK + ((chunk ^ ((row >> 2) & 3)) << 4);
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
 
 // Byte offset of tap t (row-major over kh x kw) from a pixel's tap (0, 0); uniform.
 __device__ __forceinline__ int tap_offset(const Params& p, int t) {
@@ -149,29 +119,6 @@ __device__ __forceinline__ v4i gather16(int d0, int d1, int d2, int d3) {
   return (v4i){(int)r02[0], (int)r13[0], (int)r02[1], (int)r13[1]};
 }
 
-struct CodeDst {
-  int8_t* ptr;
-  int cp, pad, hp, wp;
-};
-
-__device__ __forceinline__ void store_codes(const CodeDst& t, int n, int ho, int wo, int ch, bool ok, v4i v) {
-  if (ok && ch < t.cp)
-    *reinterpret_cast<v4i*>(t.ptr + (((int64_t)n * t.hp + ho + t.pad) * t.wp + wo + t.pad) * t.cp + ch) = v;
-}
-
-// Epilogue kinds (one kernel instantiation each, so a kernel carries only its path):
-//   EK_NCHW   mode 0: the drop-in fp32 NCHW output of QConv2d / QLinear
-//   EK_LUT    conv -> RangeBN -> ReLU -> one consumer's codes via the per-channel table
-//   EK_BNCODE conv -> RangeBN input codes only (stem before the code-domain max-pool)
-//   EK_GEN    any other fused chain: [RangeBN] [+ residual] [ReLU] -> fp32 / codes x2
-enum { EK_NCHW = 0, EK_LUT = 1, EK_BNCODE = 2, EK_GEN = 3 };
-
-static inline int epi_kind(const qnn_epilogue& e) {
-  if (e.mode == 0) return EK_NCHW;
-  if (e.lut) return EK_LUT;
-  if (e.out_bncode && !e.out_f32 && !e.out_code0 && !e.out_code1) return EK_BNCODE;
-  return EK_GEN;
-}
 
 
 // y for channels cl..cl+3 (register group g of an accumulator): the exact decomposition
@@ -196,54 +143,6 @@ __device__ __forceinline__ void conv_out4(const float* s_f, int BM, int cl, int 
   v[0] = p[0].x, v[1] = p[0].y, v[2] = p[1].x, v[3] = p[1].y;
 }
 
-// Epilogue data in LDS at p.epi_off (f32 unless noted):
-//   [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq
-//   [7BM, (7+nclass)BM) border table [cls][BM]  then (EK_LUT) int8 LUT [BM][256]
-// moved by LDS-DMA (4 bytes per lane for the vectors and the table, 16 for the LUT), one
-// job per wave-instruction, so the whole staging is ~8 DMA per wave and one round trip.
-// Channels past cout read channel cout-1 (their outputs are never stored).
-template <class C, int EK>
-__device__ __forceinline__ void stage_epi(const Params& p, const int8_t* x, int8_t* dst, int c0, int wave, int lane) {
-  constexpr int BM = C::BM, W = C::W, CH = BM / 64;  // 64-float chunks per vector
-  const qnn_epilogue& e = p.e;
-  const int cmax = p.d.cout - 1;
-  const int nvec = (EK != EK_NCHW && e.bn_mean) ? 7 : 3;
-  const int nf = (nvec + e.nclass) * CH;
-  for (int jb = wave; jb < nf; jb += W) {
-    const int v = jb / CH, k = jb - v * CH;
-    const int arr = v < nvec ? v : 7 + (v - nvec);
-    int c = c0 + 64 * k + lane;
-    c = c < cmax ? c : cmax;
-    const float* src;
-    switch (arr) {
-      case 0: src = e.sxsw; break;
-      case 1: src = e.sxbw; break;
-      case 2:  // no bias: zeros from the input's 128-byte zero page
-        if (!e.bias) {
-          src = reinterpret_cast<const float*>(x + p.d.zero_off);
-          c = lane & 31;
-        } else {
-          src = e.bias;
-        }
-        break;
-      case 3: src = e.bn_mean; break;
-      case 4: src = e.bn_sq; break;
-      case 5: src = e.bn_wq; break;
-      case 6: src = e.bn_bq; break;
-      default: src = e.table + (int64_t)(arr - 7) * p.d.cout; break;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)(src + c), (lds_ptr_t)(dst + 4 * (arr * BM + 64 * k)), 4, 0, 0);
-  }
-  if constexpr (EK == EK_LUT) {
-    int8_t* lut = dst + 4 * (7 + e.nclass) * BM;
-    for (int jl = wave; jl < BM / 4; jl += W) {
-      int c = c0 + 4 * jl + (lane >> 4);
-      c = c < cmax ? c : cmax;
-      __builtin_amdgcn_global_load_lds((const void*)(e.lut + (int64_t)c * 256 + 16 * (lane & 15)),
-                                       (lds_ptr_t)(lut + 1024 * jl), 16, 0, 0);
-    }
-  }
-}
 
 // Border-table class of each of this lane's TN pixels (computed before the main loop so
 // the hcls / wcls loads complete under it).
@@ -1284,8 +1183,6 @@ static int main_lds_bytes(int tapm, bool masked) {
   return C::NS * C::STAGE + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
 }
 
-constexpr int LDS_MAX = 160 * 1024;
-
 // LDS of a launch: main loop (lds_main bytes at 0), epilogue data (early: beside the main
 // loop's LDS, DMA'd at kernel start; late: at 0 once the main loop is done), NCHW transpose
 // scratch (after the loop).  Returns the dynamic LDS bytes, or -1 if over 160 KiB.
@@ -1457,7 +1354,7 @@ using B14 = Cfg<4, 2, 2, 2, 64, 3, 1>;
 using B15 = Cfg<1, 4, 2, 2, 64, 3, 2>;
 using B16 = Cfg<2, 2, 2, 2, 64, 3, 2>;
 using B17 = Cfg<1, 2, 2, 2, 64, 3, 4>;
-constexpr int NCFG = 18;  // 9: C6 with 2 k-steps per phase
+constexpr int NCFG = 18;  // qconv.hip configurations (9: C6 with 2 k-steps per phase); then qconv16.hip's
 struct CfgInfo {
   int bm, bn, per_cu, waves;
   float rate;  // relative MFMA throughput per CU (bytes moved per op, measured)
@@ -1473,8 +1370,11 @@ static const CfgInfo CFG[NCFG] = {
 };
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
+static int ncfg_all() { return NCFG + q16_count(); }
+
 static bool cfg_ok(int k, const Params& p) {
-  if (k < 0 || k >= NCFG) return false;
+  if (k >= NCFG) return q16_ok(k - NCFG, p);
+  if (k < 0) return false;
   const int ek = epi_kind(p.e);
   const CfgInfo& c = CFG[k];
   if (ek == EK_GEN && (k == 0 || k == 6 || k == 9 || k == 12)) return false;  // 256x256 + general chain
@@ -1487,6 +1387,7 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
+  if (k >= NCFG) return q16_cost(k - NCFG, p);
   const CfgInfo& c = CFG[k];
   const int64_t tiles = cdiv(p.M, c.bn) * cdiv(p.d.cout, c.bm);
   const int64_t slots = (int64_t)NUM_CU * c.per_cu;
@@ -1506,7 +1407,7 @@ static int pick_cfg(const Params& p) {
   if (p.d.tile > 0) return ok(p.d.tile - 1) ? p.d.tile - 1 : -1;  // explicit: built, or an argument error
   int best = -1;
   double bc = 0;
-  for (int k = 0; k < NCFG; ++k) {
+  for (int k = 0; k < ncfg_all(); ++k) {
     if (!ok(k)) continue;  // 256x256 + the general chain spills registers
     const double c = cfg_cost(k, p);
     if (best < 0 || c < bc) best = k, bc = c;
@@ -1515,6 +1416,7 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (k >= NCFG) return q16_launch(k - NCFG, x, w, p, s);
   switch (k) {
     case 0: return launch_ek<C0>(x, w, p, s);
     case 1: return launch_ek<C1>(x, w, p, s);
@@ -1583,7 +1485,7 @@ static int conv_params(const qnn_conv_desc& d, const qnn_epilogue& e, Params& p)
   return QNN_OK;
 }
 
-extern "C" int qnn_conv_tile_count(void) { return NCFG; }
+extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
 extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn,
                              int* nblk) {
@@ -1594,9 +1496,12 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   const int k = pick_cfg(p);
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
-  if (bm) *bm = CFG[k].bm;
-  if (bn) *bn = CFG[k].bn;
-  if (nblk) *nblk = (int)(cdiv(p.M, CFG[k].bn) * cdiv(p.d.cout, CFG[k].bm));
+  int tbm, tbn;
+  if (k >= NCFG) q16_tile(k - NCFG, &tbm, &tbn);
+  else tbm = CFG[k].bm, tbn = CFG[k].bn;
+  if (bm) *bm = tbm;
+  if (bn) *bn = tbn;
+  if (nblk) *nblk = (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm));
   return QNN_OK;
 }
 

@@ -1,0 +1,694 @@
+// int8 implicit-GEMM convolution on v_mfma_i32_16x16x64_i8 with LDS-staged input bands:
+// the eval forward of QConv2d / QLinear (models/modules/quantize.py:314-349, :398-428),
+// same exact decomposition and epilogue arithmetic as qconv.hip, so every
+// configuration of either file computes bitwise identical outputs.
+//
+// Why a second kernel family (measured on MI355X, profiles/r2_mfma_peak.jsonl): a stream of
+// v_mfma_i32_32x32x32_i8 holds the chip at 1.4-1.7 GHz (3.40 POPS at best), the same work as
+// v_mfma_i32_16x16x64_i8 at ~2.0 GHz (3.94 POPS); and qconv.hip's implicit im2col pulls each
+// input byte through L2 -> LDS once per tap.  Here:
+//
+// * B operand = a BAND in LDS, loaded once per K chunk (Cp up to 64 channels = one 64-byte
+//   K stage per tap): for kh x kw > 1 the padded input rows [R0, R1) the block's BN output
+//   pixels read (stride-2 rows with even columns first), for 1x1 the block's pixels
+//   themselves (any stride).  Every tap's B fragment is an LDS read at a shifted address.
+// * Band layout: PLANAR, plane g = bytes [16g, 16g+16) of every band pixel's chunk, planes
+//   1 KiB aligned.  A 16x16x64 B fragment (lane: pixel lane&15, K bytes 16*(lane>>4)..)
+//   reads plane lane>>4 at 16 consecutive band pixels: 16 distinct bank slots per
+//   ds_read_b128 lane group, no swizzle, one VALU (the tap offset add) per fragment.
+// * A operand = weights through a D-slot LDS ring, one 64-byte K stage per slot, LDS-DMA
+//   D-1 stages ahead, one s_barrier per stage.  Rows XOR-swizzled on the DMA source side
+//   (slot ^ ((row >> 2) & 1) << 1) so A fragment reads are conflict-free.
+// * sum_valid(q'_x) (the s_x*b_w term): per band pixel channel sums accumulated once per
+//   chunk, then summed over the taps per output pixel after the loop; space-to-depth stems
+//   (per-tap channel masks) accumulate masked v_dot4 of their fragments instead.
+#include <type_traits>
+
+#include "qconv_common.h"
+
+#ifndef QNN_ABLATE
+#define QNN_ABLATE 0  // diagnostic builds only (make ablate): 1 no weight loads, 2 no MFMA, 3 no epilogue
+#endif
+
+namespace qnn {
+namespace q16 {
+
+template <int WGM_, int WGN_, int TM_, int TN_, int D_, int BPC_>
+struct Cfg {
+  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, D = D_, BPC = BPC_;
+  static constexpr int W = WGM * WGN, NT = 64 * W;
+  static constexpr int BM = WGM * TM * 16, BN = WGN * TN * 16;
+  static constexpr int STAGE_A = BM * 64;
+  static constexpr int NA = BM / 16 / W;  // weight DMA (16 rows x 64 B) per wave per stage
+  static_assert(BM % (16 * W) == 0, "weight DMA rows must split evenly over the waves");
+  static_assert(BM % 64 == 0, "epilogue staging moves 64-channel groups");
+};
+
+constexpr int NBWMAX = 8;  // band DMA pieces per wave per chunk
+constexpr int PPTMAX = 4;  // band pixels per thread (channel sums)
+
+struct Band16 {
+  int list;            // 1: band pixel q = output pixel m0 + q (1x1); 0: padded input rows [R0, R1)
+  int npl, tps;        // 16-byte planes per band pixel, taps per 64-byte stage (4 / npl)
+  int nc, ns, kt;      // K chunks, stages per chunk, stages in all
+  int s2, we;          // row band of a stride-2 conv: even columns first, we = (wp + 1) / 2
+  uint32_t wp_magic;   // ceil(2^32 / wp)
+  int plane, ppp;      // LDS bytes per plane (multiple of 1 KiB), 1 KiB pieces per plane
+  int nbw;             // band DMA pieces per wave per chunk (<= NBWMAX)
+  int nbuf, bufsz;     // band buffers and their size
+  int band_off, zero_off, tap_off, s_off, mask_off;
+};
+
+__device__ __forceinline__ void wait_rt(int n) {
+  if (n >= 24) wait_vmcnt<24>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else switch (n) {
+      case 15: wait_vmcnt<15>(); break;
+      case 14: wait_vmcnt<14>(); break;
+      case 13: wait_vmcnt<13>(); break;
+      case 12: wait_vmcnt<12>(); break;
+      case 11: wait_vmcnt<11>(); break;
+      case 10: wait_vmcnt<10>(); break;
+      case 9: wait_vmcnt<9>(); break;
+      case 8: wait_vmcnt<8>(); break;
+      case 7: wait_vmcnt<7>(); break;
+      case 6: wait_vmcnt<6>(); break;
+      case 5: wait_vmcnt<5>(); break;
+      case 4: wait_vmcnt<4>(); break;
+      case 3: wait_vmcnt<3>(); break;
+      case 2: wait_vmcnt<2>(); break;
+      case 1: wait_vmcnt<1>(); break;
+      default: wait_vmcnt<0>(); break;
+    }
+}
+
+// y of 4 consecutive channels cl..cl+3 (local) of one pixel: the exact decomposition with the
+// op order of qconv.hip's conv_out4p (fma(sw, acc, fma(bw, psq, tb)) + bias), packed pairs.
+__device__ __forceinline__ void conv_out4(const float* s_f, int BM, int cl, int ptab, float psq, const v4i& a,
+                                          f2 (&v)[2]) {
+  const float4 sw = *reinterpret_cast<const float4*>(s_f + cl);
+  const float4 bw = *reinterpret_cast<const float4*>(s_f + BM + cl);
+  const float4 tb = *reinterpret_cast<const float4*>(s_f + ptab + cl);
+  const float4 bi = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
+  const f2 p2 = {psq, psq};
+  const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
+  v[0] = pfma((f2){sw.x, sw.y}, a01, pfma((f2){bw.x, bw.y}, p2, (f2){tb.x, tb.y})) + (f2){bi.x, bi.y};
+  v[1] = pfma((f2){sw.z, sw.w}, a23, pfma((f2){bw.z, bw.w}, p2, (f2){tb.z, tb.w})) + (f2){bi.z, bi.w};
+}
+
+struct Pix {  // one output pixel of a lane
+  int m, n, ho, wo;
+  bool ok;
+};
+
+// Epilogue over the 16x16 accumulator layout: acc[i][j] lane l holds channels
+// c0 + wm*16*TM + 16i + 4(l>>4) + r (r = 0..3) of pixel m0 + wn*16*TN + 16j + (l&15).
+template <class C, int EK>
+__device__ __forceinline__ void epilogue16(const Params& p, const v4i (&acc)[C::TM][C::TN], const int (&sumq)[C::TN],
+                                           const int (&pcls)[C::TN], const Pix (&pix)[C::TN], const int8_t* smem,
+                                           int c0, int wm, int lane) {
+  constexpr int BM = C::BM, TM = C::TM, TN = C::TN;
+  const qnn_conv_desc& d = p.d;
+  const qnn_epilogue& e = p.e;
+  const int g = lane >> 4;
+  const int HoWo = d.ho * d.wo;
+  const float* s_f = reinterpret_cast<const float*>(smem + p.epi_off);
+  const int nparam = 7 * BM;
+  const int8_t* s_lut = smem + p.epi_off + 4 * (7 + e.nclass) * BM;
+  const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+  const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
+  const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+  const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
+  const bool has_res = EK == EK_GEN && e.residual != nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const Pix& P = pix[j];
+    const int ptab = nparam + pcls[j] * BM;
+    const float psq = (float)sumq[j];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cl = wm * 16 * TM + 16 * i + 4 * g;  // local channel of register 0
+      const int c = c0 + cl;
+      const bool cok = c < d.cout;                   // fused modes: cout % 16 == 0 (4-channel groups all in)
+      f2 v[2];
+      conv_out4(s_f, BM, cl, ptab, psq, acc[i][j], v);
+      if constexpr (EK == EK_NCHW) {  // drop-in QConv2d output, NCHW fp32
+        if (P.ok) {
+          float* yp = e.out_f32 + ((int64_t)P.n * d.cout + c) * HoWo + P.ho * d.wo + P.wo;
+          const float y4[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c + r < d.cout) yp[(int64_t)r * HoWo] = y4[r];
+        }
+      } else if constexpr (EK == EK_LUT) {  // conv -> RangeBN -> ReLU -> consumer quantizer, tabulated
+        const f2 q0 = qclamp2(v[0], bnp) + MAGIC_U8, q1 = qclamp2(v[1], bnp) + MAGIC_U8;
+        const unsigned qq[4] = {__float_as_uint(q0.x) & 255u, __float_as_uint(q0.y) & 255u,
+                                __float_as_uint(q1.x) & 255u, __float_as_uint(q1.y) & 255u};
+        int rr = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rr |= ((int)(uint8_t)s_lut[(cl + u) * 256 + qq[u]]) << (8 * u);
+        if (P.ok && c < e.code0_cp)
+          *reinterpret_cast<int*>(e.out_code0 + (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp +
+                                                 P.wo + e.code0_pad) * e.code0_cp + c) = cok ? rr : 0;
+      } else if constexpr (EK == EK_BNCODE) {
+        const int rr = pack4(qclamp2(v[0], bnp) + MAGIC_U8, qclamp2(v[1], bnp) + MAGIC_U8);
+        if (P.ok && cok) *reinterpret_cast<int*>(e.out_bncode + (int64_t)P.m * d.cout + c) = rr;
+      } else {  // EK_GEN: [RangeBN] [+ residual] [ReLU] -> fp32 and/or codes x2
+        if (e.bn_mean) {
+          const f2 qb[2] = {qclamp2(v[0], bnp), qclamp2(v[1], bnp)};
+          const float4 mn4 = *reinterpret_cast<const float4*>(s_f + 3 * BM + cl);
+          const float4 sq4 = *reinterpret_cast<const float4*>(s_f + 4 * BM + cl);
+          const float4 wq4 = *reinterpret_cast<const float4*>(s_f + 5 * BM + cl);
+          const float4 bq4 = *reinterpret_cast<const float4*>(s_f + 6 * BM + cl);
+          const f2 mn[2] = {{mn4.x, mn4.y}, {mn4.z, mn4.w}}, sq[2] = {{sq4.x, sq4.y}, {sq4.z, sq4.w}};
+          const f2 wq[2] = {{wq4.x, wq4.y}, {wq4.z, wq4.w}}, bq[2] = {{bq4.x, bq4.y}, {bq4.z, bq4.w}};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f2 o = rint2(qb[h]) * bn_s2;  // dequant: q * s
+            o = o + bn_m2;                // + min
+            o = o - mn[h];                // x - mean
+            o = o * sq[h];                // * q(scale)
+            o = o * wq[h];                // * q(weight)
+            v[h] = o + bq[h];             // + q(bias)
+          }
+        }
+        const int mc = P.ok ? P.m : p.M - 1;
+        const int cc = cok ? c : d.cout - 4;
+        if (has_res) {
+          const int64_t fi = e.f32_tiled ? ctile_index(mc, cc, p.ct) : (int64_t)mc * d.cout + cc;
+          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + fi);
+          v[0] = v[0] + (f2){r4.x, r4.y};
+          v[1] = v[1] + (f2){r4.z, r4.w};
+        }
+        if (e.relu) {
+          v[0].x = fmaxf(v[0].x, 0.f); v[0].y = fmaxf(v[0].y, 0.f);
+          v[1].x = fmaxf(v[1].x, 0.f); v[1].y = fmaxf(v[1].y, 0.f);
+        }
+        if (e.out_f32 && P.ok && cok) {
+          const int64_t fi = e.f32_tiled ? ctile_index(P.m, c, p.ct) : (int64_t)P.m * d.cout + c;
+          *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+        }
+        if (e.out_code0 && P.ok && c < e.code0_cp) {
+          const int k0 = cok ? pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8) : 0;
+          *reinterpret_cast<int*>(e.out_code0 + (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp +
+                                                 P.wo + e.code0_pad) * e.code0_cp + c) = k0;
+        }
+        if (e.out_code1 && P.ok && c < e.code1_cp) {
+          const int k1 = cok ? pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8) : 0;
+          *reinterpret_cast<int*>(e.out_code1 + (((int64_t)P.n * e.code1_hp + P.ho + e.code1_pad) * e.code1_wp +
+                                                 P.wo + e.code1_pad) * e.code1_cp + c) = k1;
+        }
+      }
+    }
+  }
+}
+
+template <class C, int EK, bool MASKED>
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv16_kernel(
+    const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Band16 b) {
+  constexpr int BM = C::BM, BN = C::BN, W = C::W, TM = C::TM, TN = C::TN, D = C::D, NA = C::NA, NT = C::NT;
+  constexpr int STAGE_A = C::STAGE_A;
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  const int px = lane & 15, g = lane >> 4;
+
+  // ---- XCD-aware bijective block -> tile map (channel tiles fastest: blocks sharing a band share L2)
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nbx = (p.M + BN - 1) / BN;
+  const int nblk = nbx * nby;
+  int t;
+  {
+    const int bb = blockIdx.x, xcd = bb & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bb >> 3);
+  }
+  const int m0 = (t / nby) * BN;
+  const int c0 = (t % nby) * BM;
+  const int HoWo = d.ho * d.wo;
+  auto decode = [&](int m, Pix& P) {
+    P.m = m;
+    P.n = m / HoWo;
+    const int r = m - P.n * HoWo;
+    P.ho = r / d.wo;
+    P.wo = r - P.ho * d.wo;
+  };
+  const int mlast = (m0 + BN < p.M ? m0 + BN : p.M) - 1;
+  int R0 = 0, NBP;
+  {
+    Pix a, z;
+    decode(m0, a);
+    decode(mlast, z);
+    if (b.list) {
+      NBP = mlast - m0 + 1;
+    } else {
+      R0 = a.n * d.hp + a.ho * d.sh;
+      NBP = (z.n * d.hp + z.ho * d.sh + d.kh - R0) * d.wp;
+    }
+  }
+  R0 = __builtin_amdgcn_readfirstlane(R0);
+  NBP = __builtin_amdgcn_readfirstlane(NBP);
+
+  // ---- LDS constants: zero bytes, tap offsets (band pixels; padded taps -> tap 0), K mask
+  int* s_tap = reinterpret_cast<int*>(smem + b.tap_off);
+  if (tid < 4) *reinterpret_cast<v4i*>(smem + b.zero_off + 16 * tid) = (v4i){0, 0, 0, 0};
+  if (tid < 64) {
+    int dl = 0;
+    if (tid < p.taps && !b.list) {
+      const int tr = tid / d.kw, tc = tid - tr * d.kw;
+      dl = tr * d.wp + (b.s2 ? (tc & 1) * b.we + (tc >> 1) : tc);
+    }
+    s_tap[tid] = dl;
+  }
+  if constexpr (MASKED) {
+    for (int i = tid; i < d.kpad / 16; i += NT)
+      *reinterpret_cast<v4i*>(smem + b.mask_off + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
+  }
+  __syncthreads();  // before any LDS-DMA is in flight (a barrier then would drain it)
+
+  // ---- this lane's pixels: band pixel of tap 0 (x16 = byte offset within a plane)
+  Pix pix[TN];
+  int bq16[TN];
+  {
+    Pix last;
+    decode(p.M - 1, last);
+    Pix cur;
+    const int mb = m0 + wn * 16 * TN + px;
+    decode(mb < p.M ? mb : p.M - 1, cur);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int m = mb + 16 * j;
+      Pix P = cur;
+      P.m = m;
+      P.ok = m < p.M;
+      if (!P.ok) P = last, P.ok = false;
+      pix[j] = P;
+      int q;
+      if (b.list) q = (P.ok ? m : p.M - 1) - m0;
+      else q = (P.n * d.hp + P.ho * d.sh - R0) * d.wp + P.wo;  // column wo*sw: wo itself (stride 2: even half)
+      bq16[j] = 16 * q;
+      // next pixel of this lane: +16
+      cur.wo += 16;
+      while (cur.wo >= d.wo) {
+        cur.wo -= d.wo;
+        if (++cur.ho == d.ho) cur.ho = 0, ++cur.n;
+      }
+    }
+  }
+  const int tsub = b.npl == 4 ? 0 : (b.npl == 2 ? g >> 1 : g);  // which tap of a stage this lane's bytes hold
+  const int lpo = (g & (b.npl - 1)) * b.plane;                    // this lane's plane
+
+  // ---- weights: 16 rows x 64 B per DMA, slots XOR-swizzled by row bit 2 (source side)
+  const int8_t* wblk = w + (int64_t)c0 * d.kpad;
+  uint32_t aoff[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int row = 16 * (wave + W * j) + (lane >> 2);
+    const int crow = (c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0);
+    aoff[j] = (uint32_t)(crow * d.kpad + 16 * ((lane & 3) ^ (((row >> 2) & 1) << 1)));
+  }
+  const int offa = (wm * 16 * TM + px) * 64 + 16 * (g ^ (((px >> 2) & 1) << 1));
+
+  // ---- band DMA sources of this lane's pieces (fixed across chunks; + 16*npl*c per chunk)
+  uint32_t bsrc[NBWMAX];
+#pragma unroll
+  for (int k = 0; k < NBWMAX; ++k) {
+    bsrc[k] = 0;
+    if (k < b.nbw) {
+      const int piece = wave + W * k;
+      int pl = piece / b.ppp;
+      pl = pl < b.npl ? pl : b.npl - 1;  // slack pieces past the last plane re-read valid bytes
+      int q = (piece - (piece / b.ppp) * b.ppp) * 64 + lane;
+      q = q < NBP ? q : NBP - 1;
+      int gp;
+      if (b.list) {
+        Pix P;
+        decode(m0 + q, P);
+        gp = (P.n * d.hp + P.ho * d.sh) * d.wp + P.wo * d.sw;
+      } else {
+        const int r = (int)__umulhi((uint32_t)q, b.wp_magic);
+        const int ci = q - r * d.wp;
+        const int col = b.s2 ? (ci < b.we ? 2 * ci : 2 * (ci - b.we) + 1) : ci;
+        gp = (R0 + r) * d.wp + col;
+      }
+      bsrc[k] = (uint32_t)(gp * d.cp + 16 * pl);
+    }
+  }
+
+  int pcls[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) pcls[j] = p.e.hcls[pix[j].ho] * p.e.nwc + p.e.wcls[pix[j].wo];
+  if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
+
+  // ---- DMA issue
+  auto issue_band = [&](int c, int bi) {
+    int8_t* dst = smem + b.band_off + bi * b.bufsz;
+    const uint32_t co = (uint32_t)(c * 16 * b.npl);
+#pragma unroll
+    for (int k = 0; k < NBWMAX; ++k) {
+      if (k < b.nbw) {
+        uint32_t off = bsrc[k] + co;
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(dst + (wave + W * k) * 1024), 16, 0, 0);
+      }
+    }
+  };
+  auto issue_w = [&](int c, int s, int slot) {
+    if (QNN_ABLATE == 1) return;
+    const uint32_t ko = (uint32_t)(b.npl == 4 ? s * d.cp + 64 * c : 64 * s);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      uint32_t off = aoff[j] + ko;
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(smem + slot * STAGE_A + (wave + W * j) * 1024),
+                                       16, 0, 0);
+    }
+  };
+  const int KT = b.kt;
+  int ik = 0, ic = 0, is = 0, ib = 0;  // next stage to issue
+  auto issue_stage = [&](int slot) {
+    if (ik < KT) {
+      if (is == 0) issue_band(ic, ib);
+      issue_w(ic, is, slot);
+      if (++is == b.ns) {
+        is = 0, ++ic;
+        if (++ib == b.nbuf) ib = 0;
+      }
+    } else {
+      issue_w(b.nc - 1, b.ns - 1, slot);  // clamped: keeps every wave's DMA count uniform
+    }
+    ++ik;
+  };
+
+  v4i acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+  int sumq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) sumq[j] = 0;
+  int sacc[PPTMAX];
+#pragma unroll
+  for (int u = 0; u < PPTMAX; ++u) sacc[u] = 0;
+
+  auto compute = [&](auto slotc, int bi, int s) {
+    constexpr int AO = decltype(slotc)::value * STAGE_A;
+    v4i fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const v4i*>(smem + AO + offa + i * 1024);
+    const int base = b.band_off + bi * b.bufsz + lpo + 16 * s_tap[s * b.tps + tsub];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const v4i*>(smem + base + bq16[j]);
+    if constexpr (MASKED) {
+      const v4i mk = *reinterpret_cast<const v4i*>(smem + b.mask_off + 64 * s + 16 * g);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int sm = __builtin_amdgcn_sdot4(fb[j].x, mk.x, sumq[j], false);
+        sm = __builtin_amdgcn_sdot4(fb[j].y, mk.y, sm, false);
+        sm = __builtin_amdgcn_sdot4(fb[j].z, mk.z, sm, false);
+        sumq[j] = __builtin_amdgcn_sdot4(fb[j].w, mk.w, sm, false);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (QNN_ABLATE == 2) {
+          asm volatile("" ::"v"(fa[i]), "v"(fb[j]));
+          acc[i][j][0] += fa[i].x;
+        } else {
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      }
+  };
+  // channel sums of the band chunk in buffer bi (every band pixel, all planes)
+  auto band_sums = [&](int bi) {
+    const int8_t* bb = smem + b.band_off + bi * b.bufsz;
+    const int ones = 0x01010101;
+#pragma unroll
+    for (int u = 0; u < PPTMAX; ++u) {
+      const int q = tid + NT * u;
+      if (q < NBP) {
+        int s = sacc[u];
+        for (int pl = 0; pl < b.npl; ++pl) {
+          const v4i v = *reinterpret_cast<const v4i*>(bb + pl * b.plane + 16 * q);
+          s = __builtin_amdgcn_sdot4(v.x, ones, s, false);
+          s = __builtin_amdgcn_sdot4(v.y, ones, s, false);
+          s = __builtin_amdgcn_sdot4(v.z, ones, s, false);
+          s = __builtin_amdgcn_sdot4(v.w, ones, s, false);
+        }
+        sacc[u] = s;
+      }
+    }
+  };
+
+  // ---- prologue: stages 0 .. D-2 in flight
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) issue_stage(k);
+  // Stage k = (c, s) lives in weight slot k % D, its chunk's band in buffer bi.  Before the
+  // barrier of stage k each wave waits for its own DMA of stage k; the younger ones (stages
+  // k+1 .. k+D-2: weights, plus a band chunk where such a stage opens a chunk) stay in flight.
+  int c = 0, s = 0, bi = 0;
+  auto step = [&](auto slotc, int k) {
+    constexpr int SL = decltype(slotc)::value;
+    int younger = 0;
+#pragma unroll
+    for (int dk = 1; dk <= D - 2; ++dk)
+      younger += NA + ((k + dk < KT && (s + dk) % b.ns == 0) ? b.nbw : 0);
+    wait_rt(younger);
+    __builtin_amdgcn_s_barrier();
+    issue_stage((SL + D - 1) % D);
+    if constexpr (!MASKED)
+      if (s == 0) band_sums(bi);
+    compute(slotc, bi, s);
+    if (++s == b.ns) {
+      s = 0, ++c;
+      if (++bi == b.nbuf) bi = 0;
+    }
+  };
+  for (int k = 0; k < KT; k += D) {
+    step(std::integral_constant<int, 0>{}, k);
+    if (k + 1 < KT) step(std::integral_constant<int, 1>{}, k + 1);
+    if (k + 2 < KT) step(std::integral_constant<int, 2>{}, k + 2);
+    if constexpr (D == 4)
+      if (k + 3 < KT) step(std::integral_constant<int, 3>{}, k + 3);
+  }
+  wait_vmcnt<0>();  // the clamped tail DMAs still write LDS
+
+  // ---- sum_valid(q'_x) per output pixel
+  if constexpr (MASKED) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      sumq[j] += __shfl_xor(sumq[j], 16, 64);
+      sumq[j] += __shfl_xor(sumq[j], 32, 64);
+    }
+  } else {
+    int* s_S = reinterpret_cast<int*>(smem + b.s_off);
+#pragma unroll
+    for (int u = 0; u < PPTMAX; ++u) {
+      const int q = tid + NT * u;
+      if (q < NBP) s_S[q] = sacc[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int sm = 0;
+      const int q = bq16[j] >> 4;
+      for (int tt = 0; tt < p.taps; ++tt) sm += s_S[q + s_tap[tt]];
+      sumq[j] = sm;
+    }
+  }
+  __syncthreads();  // main-loop LDS is reused by the epilogue
+  if (QNN_ABLATE == 3) {
+    int z = sumq[0];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z ^= acc[i][j][r];
+    if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;
+    return;
+  }
+  if (!p.epi_early) {
+    stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+  epilogue16<C, EK>(p, acc, sumq, pcls, pix, smem, c0, wm, lane);
+}
+
+// ------------------------------------------------------------------ host side
+// Fills the band plan; returns the main-loop LDS bytes, or -1 if the layer / tile does not fit.
+static int band16(const Params& p, int BM, int BN, int nt, int D, int bpc, Band16& b) {
+  const qnn_conv_desc& d = p.d;
+  if (d.sh != d.sw || (d.sh != 1 && d.sh != 2)) return -1;
+  const int npl = d.cp >= 64 ? 4 : d.cp / 16;
+  if (d.kmask && npl != 1) return -1;
+  b.npl = npl;
+  b.tps = 4 / npl;
+  const int taps_pad = (p.taps + b.tps - 1) / b.tps * b.tps;
+  if (taps_pad > 64) return -1;
+  b.nc = npl == 4 ? d.cp / 64 : 1;
+  b.ns = taps_pad / b.tps;
+  b.kt = b.nc * b.ns;
+  if ((npl < 4 ? b.ns * 64 : p.taps * d.cp) > d.kpad) return -1;
+  b.list = p.taps == 1;
+  b.s2 = !b.list && d.sh == 2;
+  b.we = (d.wp + 1) / 2;
+  b.wp_magic = (uint32_t)((0x100000000ULL + (uint64_t)d.wp - 1) / (uint64_t)d.wp);
+  int64_t nbp;
+  if (b.list) {
+    nbp = BN;
+  } else {  // BN consecutive output pixels span at most RO + 1 output rows and `cross` image boundaries
+    const int RO = (BN + d.wo - 2) / d.wo;
+    const int cross = (d.ho - 1 + RO) / d.ho;
+    nbp = (int64_t)(RO * d.sh + cross * (d.hp - d.ho * d.sh) + d.kh) * d.wp;
+  }
+  if (nbp > PPTMAX * nt) return -1;
+  b.plane = (int)cdiv(nbp * 16, 1024) * 1024;
+  b.ppp = b.plane / 1024;
+  const int W = nt / 64;
+  b.nbw = (int)cdiv(npl * b.ppp, W);
+  if (b.nbw > NBWMAX) return -1;
+  b.bufsz = b.nbw * W * 1024;
+  b.nbuf = std::min(b.nc, 1 + (int)cdiv(D - 1, b.ns));
+  b.band_off = D * BM * 64;
+  b.zero_off = b.band_off + b.nbuf * b.bufsz;
+  b.tap_off = b.zero_off + 64;
+  b.s_off = b.tap_off + 256;
+  b.mask_off = b.s_off + (int)nbp * 4;
+  const int lds = b.mask_off + (d.kmask ? d.kpad : 0);
+  if (lds > LDS_MAX / bpc) return -1;
+  return lds;
+}
+
+template <class C>
+static int plan_lds(int lds_main, Params& q) {
+  lds_main = (lds_main + 15) & ~15;
+  const int k = epi_kind(q.e);
+  const int epi = 4 * (7 + q.e.nclass) * C::BM + (k == EK_LUT ? 256 * C::BM : 0);
+  int lds;
+  if (lds_main + epi <= LDS_MAX / C::BPC) {
+    q.epi_early = 1, q.epi_off = lds_main;
+    lds = lds_main + epi;
+  } else {
+    q.epi_early = 0, q.epi_off = 0;
+    lds = epi > lds_main ? epi : lds_main;
+  }
+  q.scr_off = 0;
+  return lds > LDS_MAX ? -1 : lds;
+}
+
+template <class C, int EK, bool MASKED>
+static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  auto kern = qconv16_kernel<C, EK, MASKED>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  Band16 b;
+  const int main = band16(p, C::BM, C::BN, C::NT, C::D, C::BPC, b);
+  if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
+  Params q = p;
+  const int lds = plan_lds<C>(main, q);
+  if (lds < 0) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+  const int nblk = (int)(cdiv(p.M, C::BN) * cdiv(p.d.cout, C::BM));
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q, b);
+  return QNN_OK;
+}
+
+template <class C, int EK>
+static int launch_m(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (p.d.kmask) {
+    if constexpr (C::BM == 64) return launch<C, EK, true>(x, w, p, s);
+    else return arg_error("tile configuration not built for this layer / epilogue kind");
+  }
+  return launch<C, EK, false>(x, w, p, s);
+}
+
+template <class C>
+static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  switch (epi_kind(p.e)) {
+    case EK_NCHW: return launch_m<C, EK_NCHW>(x, w, p, s);
+    case EK_LUT: return launch_m<C, EK_LUT>(x, w, p, s);
+    case EK_BNCODE: return launch_m<C, EK_BNCODE>(x, w, p, s);
+    default:
+      if constexpr (C::TM * C::TN > 16) return arg_error("tile configuration not built for this layer / epilogue kind");
+      else return launch_m<C, EK_GEN>(x, w, p, s);
+  }
+}
+
+//   id   block (cout x px)   waves (each)          blocks/CU
+//   0    256 x 256           8 (64 x 128)          1
+//   1    256 x 208           8 (32 x 208)          1   (one 14x14 image + 12 px: 241 tiles for R50 l3)
+//   2    128 x 256           8 (64 x 64)           1
+//   3    256 x 128           8 (64 x 64)           1
+//   4     64 x 256           4 (64 x 64)           2
+//   5    128 x 128           4 (64 x 64)           2
+//   6     64 x 128           4 (64 x 32)           4
+//   7     64 x 128           2 (64 x 64)           4
+using Q0 = Cfg<4, 2, 4, 8, 3, 1>;
+using Q1 = Cfg<8, 1, 2, 13, 3, 1>;
+using Q2 = Cfg<2, 4, 4, 4, 3, 1>;
+using Q3 = Cfg<4, 2, 4, 4, 3, 1>;
+using Q4 = Cfg<1, 4, 4, 4, 3, 2>;
+using Q5 = Cfg<2, 2, 4, 4, 3, 2>;
+using Q6 = Cfg<1, 4, 4, 2, 3, 4>;
+using Q7 = Cfg<1, 2, 4, 4, 3, 4>;
+constexpr int NQ = 8;
+struct Info {
+  int bm, bn, nt, bpc, acc_tiles;
+  float rate;
+};
+static const Info INFO[NQ] = {
+    {256, 256, 512, 1, 32, 2.00f}, {256, 208, 512, 1, 26, 1.95f}, {128, 256, 512, 1, 16, 1.75f},
+    {256, 128, 512, 1, 16, 1.75f}, {64, 256, 256, 2, 16, 1.50f},  {128, 128, 256, 2, 16, 1.50f},
+    {64, 128, 256, 4, 8, 1.20f},   {64, 128, 128, 4, 16, 1.10f},
+};
+
+}  // namespace q16
+
+int q16_count() { return q16::NQ; }
+
+void q16_tile(int k, int* bm, int* bn) {
+  *bm = q16::INFO[k].bm;
+  *bn = q16::INFO[k].bn;
+}
+
+bool q16_ok(int k, const Params& p) {
+  using namespace q16;
+  if (k < 0 || k >= NQ) return false;
+  const Info& f = INFO[k];
+  if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;
+  if (p.d.kmask && f.bm != 64) return false;
+  Band16 b;
+  return band16(p, f.bm, f.bn, f.nt, 3, f.bpc, b) >= 0;
+}
+
+double q16_cost(int k, const Params& p) {
+  const q16::Info& c = q16::INFO[k];
+  const int64_t tiles = cdiv(p.M, c.bn) * cdiv(p.d.cout, c.bm);
+  const int64_t slots = (int64_t)NUM_CU * c.bpc;
+  const int64_t rounds = cdiv(tiles, slots);
+  const double share = tiles < slots ? (double)cdiv(tiles, NUM_CU) : (double)c.bpc;
+  return (double)rounds * share * c.bm * c.bn * p.d.kpad / c.rate;
+}
+
+int q16_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  using namespace q16;
+  switch (k) {
+    case 0: return launch_ek<Q0>(x, w, p, s);
+    case 1: return launch_ek<Q1>(x, w, p, s);
+    case 2: return launch_ek<Q2>(x, w, p, s);
+    case 3: return launch_ek<Q3>(x, w, p, s);
+    case 4: return launch_ek<Q4>(x, w, p, s);
+    case 5: return launch_ek<Q5>(x, w, p, s);
+    case 6: return launch_ek<Q6>(x, w, p, s);
+    default: return launch_ek<Q7>(x, w, p, s);
+  }
+}
+
+}  // namespace qnn
