@@ -268,10 +268,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   }
   __syncthreads();  // before any LDS-DMA is in flight (a barrier then would drain it)
 
-  // ---- this lane's pixels: band pixel of tap 0 (x16 = byte offset within a plane)
-  Pix pix[TN];
-  int bq16[TN];
-  {
+  // ---- this lane's pixels (column tile j: m0 + wn*16*TN + 16j + lane&15): decoded with
+  // one division, then stepped by 16; pixels past M stand in for the last one (not stored)
+  auto lane_pixels = [&](Pix (&pix)[TN]) {
     Pix last;
     decode(p.M - 1, last);
     Pix cur;
@@ -285,16 +284,23 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       P.ok = m < p.M;
       if (!P.ok) P = last, P.ok = false;
       pix[j] = P;
-      int q;
-      if (b.list) q = (P.ok ? m : p.M - 1) - m0;
-      else q = (P.n * d.hp + P.ho * d.sh - R0) * d.wp + P.wo;  // column wo*sw: wo itself (stride 2: even half)
-      bq16[j] = 16 * q;
-      // next pixel of this lane: +16
       cur.wo += 16;
       while (cur.wo >= d.wo) {
         cur.wo -= d.wo;
         if (++cur.ho == d.ho) cur.ho = 0, ++cur.n;
       }
+    }
+  };
+  int bq16[TN];  // byte offset within a band plane of each column tile's pixel (tap 0)
+  {
+    Pix pix[TN];
+    lane_pixels(pix);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const Pix& P = pix[j];
+      const int q = b.list ? (P.ok ? P.m : p.M - 1) - m0
+                           : (P.n * d.hp + P.ho * d.sh - R0) * d.wp + P.wo;  // column wo*sw: wo (stride 2: even half)
+      bq16[j] = 16 * q;
     }
   }
   const int tsub = b.npl == 4 ? 0 : (b.npl == 2 ? g >> 1 : g);  // which tap of a stage this lane's bytes hold
@@ -337,9 +343,6 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     }
   }
 
-  int pcls[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) pcls[j] = p.e.hcls[pix[j].ho] * p.e.nwc + p.e.wcls[pix[j].wo];
   if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
 
   // ---- DMA issue
@@ -394,14 +397,23 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
 #pragma unroll
   for (int u = 0; u < PPTMAX; ++u) sacc[u] = 0;
 
-  auto compute = [&](auto slotc, int bi, int s) {
+  // band offset (pixels) of stage s's tap for this lane's K bytes (uniform when npl == 4)
+  auto tap_of = [&](int s) -> int {
+    if (b.list) return 0;
+    int tt = s * b.tps + tsub;
+    if (tt >= p.taps) tt = 0;  // padded taps: any valid band bytes (their weights are 0, masked in sums)
+    const int tr = (tt * p.kw_magic) >> 16, tc = tt - tr * d.kw;
+    return tr * d.wp + (b.s2 ? (tc & 1) * b.we + (tc >> 1) : tc);
+  };
+  auto read_frags = [&](auto slotc, int bi, int s, v4i (&fa)[TM], v4i (&fb)[TN]) {
     constexpr int AO = decltype(slotc)::value * STAGE_A;
-    v4i fa[TM], fb[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const v4i*>(smem + AO + offa + i * 1024);
-    const int base = b.band_off + bi * b.bufsz + lpo + 16 * s_tap[s * b.tps + tsub];
+    const int base = b.band_off + bi * b.bufsz + lpo + 16 * tap_of(s);
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const v4i*>(smem + base + bq16[j]);
+  };
+  auto mma = [&](const v4i (&fa)[TM], const v4i (&fb)[TN], int s) {
     if constexpr (MASKED) {
       const v4i mk = *reinterpret_cast<const v4i*>(smem + b.mask_off + 64 * s + 16 * g);
 #pragma unroll
@@ -412,6 +424,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
         sumq[j] = __builtin_amdgcn_sdot4(fb[j].w, mk.w, sm, false);
       }
     }
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -423,6 +436,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
           acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
       }
+    __builtin_amdgcn_s_setprio(0);
   };
   // channel sums of the band chunk in buffer bi (every band pixel, all planes)
   auto band_sums = [&](int bi) {
@@ -432,49 +446,67 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     for (int u = 0; u < PPTMAX; ++u) {
       const int q = tid + NT * u;
       if (q < NBP) {
-        int s = sacc[u];
+        int sm = sacc[u];
         for (int pl = 0; pl < b.npl; ++pl) {
           const v4i v = *reinterpret_cast<const v4i*>(bb + pl * b.plane + 16 * q);
-          s = __builtin_amdgcn_sdot4(v.x, ones, s, false);
-          s = __builtin_amdgcn_sdot4(v.y, ones, s, false);
-          s = __builtin_amdgcn_sdot4(v.z, ones, s, false);
-          s = __builtin_amdgcn_sdot4(v.w, ones, s, false);
+          sm = __builtin_amdgcn_sdot4(v.x, ones, sm, false);
+          sm = __builtin_amdgcn_sdot4(v.y, ones, sm, false);
+          sm = __builtin_amdgcn_sdot4(v.z, ones, sm, false);
+          sm = __builtin_amdgcn_sdot4(v.w, ones, sm, false);
         }
-        sacc[u] = s;
+        sacc[u] = sm;
       }
     }
   };
+  // DMA groups younger than stage k's: stages k+1 .. k+n (weights, + band where one opens a chunk)
+  auto younger = [&](int k, int s, int from, int to) {
+    int n = 0;
+#pragma unroll
+    for (int dk = from; dk <= to; ++dk) n += NA + ((k + dk < KT && (s + dk) % b.ns == 0) ? b.nbw : 0);
+    return n;
+  };
 
-  // ---- prologue: stages 0 .. D-2 in flight
+  // ---- software pipeline.  Stage k = (c, s) lives in weight slot k % D and its chunk's band
+  // buffer.  Its fragments are read one stage early (while stage k-1's MFMAs run), so the
+  // wait + barrier before that read covers stage k's DMA: at step k each wave waits for its
+  // own DMA of stage k+1 (issued D-2 steps earlier; stages k+2 .. k+D-2 stay in flight),
+  // passes the barrier, refills the slot of stage k-1 (read during step k-2) with stage
+  // k+D-1, reads stage k+1's fragments, then runs stage k's MFMAs.
+  static_assert(D == 4, "pipelined ring: 4 slots");
+  v4i fa0[TM], fb0[TN], fa1[TM], fb1[TN];
 #pragma unroll
   for (int k = 0; k < D - 1; ++k) issue_stage(k);
-  // Stage k = (c, s) lives in weight slot k % D, its chunk's band in buffer bi.  Before the
-  // barrier of stage k each wave waits for its own DMA of stage k; the younger ones (stages
-  // k+1 .. k+D-2: weights, plus a band chunk where such a stage opens a chunk) stay in flight.
-  int c = 0, s = 0, bi = 0;
+  wait_rt(younger(0, 0, 1, D - 2));
+  __builtin_amdgcn_s_barrier();
+  if constexpr (!MASKED) band_sums(0);
+  read_frags(std::integral_constant<int, 0>{}, 0, 0, fa0, fb0);
+  int s = 0;                                        // current stage's s
+  int s1 = b.ns > 1 ? 1 : 0, bi1 = b.ns > 1 ? 0 : (b.nbuf > 1 ? 1 : 0);  // next stage's s and band buffer
   auto step = [&](auto slotc, int k) {
     constexpr int SL = decltype(slotc)::value;
-    int younger = 0;
-#pragma unroll
-    for (int dk = 1; dk <= D - 2; ++dk)
-      younger += NA + ((k + dk < KT && (s + dk) % b.ns == 0) ? b.nbw : 0);
-    wait_rt(younger);
-    __builtin_amdgcn_s_barrier();
-    issue_stage((SL + D - 1) % D);
-    if constexpr (!MASKED)
-      if (s == 0) band_sums(bi);
-    compute(slotc, bi, s);
-    if (++s == b.ns) {
-      s = 0, ++c;
-      if (++bi == b.nbuf) bi = 0;
+    constexpr int NX = (SL + 1) % D;
+    if (k + 1 < KT) {
+      wait_rt(younger(k, s, 2, D - 2));
+      __builtin_amdgcn_s_barrier();
+      issue_stage((SL + D - 1) % D);
+      if constexpr (!MASKED)
+        if (s1 == 0) band_sums(bi1);
+      if constexpr ((SL & 1) == 0) read_frags(std::integral_constant<int, NX>{}, bi1, s1, fa1, fb1);
+      else read_frags(std::integral_constant<int, NX>{}, bi1, s1, fa0, fb0);
+    }
+    if constexpr ((SL & 1) == 0) mma(fa0, fb0, s);
+    else mma(fa1, fb1, s);
+    s = s1;
+    if (++s1 == b.ns) {
+      s1 = 0;
+      if (++bi1 == b.nbuf) bi1 = 0;
     }
   };
   for (int k = 0; k < KT; k += D) {
     step(std::integral_constant<int, 0>{}, k);
     if (k + 1 < KT) step(std::integral_constant<int, 1>{}, k + 1);
     if (k + 2 < KT) step(std::integral_constant<int, 2>{}, k + 2);
-    if constexpr (D == 4)
-      if (k + 3 < KT) step(std::integral_constant<int, 3>{}, k + 3);
+    if (k + 3 < KT) step(std::integral_constant<int, 3>{}, k + 3);
   }
   wait_vmcnt<0>();  // the clamped tail DMAs still write LDS
 
@@ -518,7 +550,14 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     wait_vmcnt<0>();
     __syncthreads();
   }
-  epilogue16<C, EK>(p, acc, sumq, pcls, pix, smem, c0, wm, lane);
+  {
+    Pix pix[TN];
+    lane_pixels(pix);
+    int pcls[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) pcls[j] = p.e.hcls[pix[j].ho] * p.e.nwc + p.e.wcls[pix[j].wo];
+    epilogue16<C, EK>(p, acc, sumq, pcls, pix, smem, c0, wm, lane);
+  }
 }
 
 // ------------------------------------------------------------------ host side
@@ -555,7 +594,9 @@ static int band16(const Params& p, int BM, int BN, int nt, int D, int bpc, Band1
   b.nbw = (int)cdiv(npl * b.ppp, W);
   if (b.nbw > NBWMAX) return -1;
   b.bufsz = b.nbw * W * 1024;
-  b.nbuf = std::min(b.nc, 1 + (int)cdiv(D - 1, b.ns));
+  b.nbuf = 2;  // a chunk's band is refilled D-1 stages before its first read: nbuf * ns > ns + D - 3
+  while (b.nbuf * b.ns <= b.ns + D - 3) ++b.nbuf;
+  b.nbuf = std::min(b.nc, b.nbuf);
   b.band_off = D * BM * 64;
   b.zero_off = b.band_off + b.nbuf * b.bufsz;
   b.tap_off = b.zero_off + 64;
@@ -622,29 +663,29 @@ static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStrea
 }
 
 //   id   block (cout x px)   waves (each)          blocks/CU
-//   0    256 x 256           8 (64 x 128)          1
-//   1    256 x 208           8 (32 x 208)          1   (one 14x14 image + 12 px: 241 tiles for R50 l3)
+//   0    256 x 256           4 (64 x 256)          1   (one wave per SIMD: 512-register budget)
+//   1    256 x 208           4 (64 x 208)          1   (one 14x14 image + 12 px: 242 tiles for R50 l3)
 //   2    128 x 256           8 (64 x 64)           1
 //   3    256 x 128           8 (64 x 64)           1
 //   4     64 x 256           4 (64 x 64)           2
 //   5    128 x 128           4 (64 x 64)           2
 //   6     64 x 128           4 (64 x 32)           4
 //   7     64 x 128           2 (64 x 64)           4
-using Q0 = Cfg<4, 2, 4, 8, 3, 1>;
-using Q1 = Cfg<8, 1, 2, 13, 3, 1>;
-using Q2 = Cfg<2, 4, 4, 4, 3, 1>;
-using Q3 = Cfg<4, 2, 4, 4, 3, 1>;
-using Q4 = Cfg<1, 4, 4, 4, 3, 2>;
-using Q5 = Cfg<2, 2, 4, 4, 3, 2>;
-using Q6 = Cfg<1, 4, 4, 2, 3, 4>;
-using Q7 = Cfg<1, 2, 4, 4, 3, 4>;
+using Q0 = Cfg<4, 1, 4, 16, 4, 1>;
+using Q1 = Cfg<4, 1, 4, 13, 4, 1>;
+using Q2 = Cfg<2, 4, 4, 4, 4, 1>;
+using Q3 = Cfg<4, 2, 4, 4, 4, 1>;
+using Q4 = Cfg<1, 4, 4, 4, 4, 2>;
+using Q5 = Cfg<2, 2, 4, 4, 4, 2>;
+using Q6 = Cfg<1, 4, 4, 2, 4, 4>;
+using Q7 = Cfg<1, 2, 4, 4, 4, 4>;
 constexpr int NQ = 8;
 struct Info {
   int bm, bn, nt, bpc, acc_tiles;
   float rate;
 };
 static const Info INFO[NQ] = {
-    {256, 256, 512, 1, 32, 2.00f}, {256, 208, 512, 1, 26, 1.95f}, {128, 256, 512, 1, 16, 1.75f},
+    {256, 256, 256, 1, 64, 2.00f}, {256, 208, 256, 1, 52, 1.95f}, {128, 256, 512, 1, 16, 1.75f},
     {256, 128, 512, 1, 16, 1.75f}, {64, 256, 256, 2, 16, 1.50f},  {128, 128, 256, 2, 16, 1.50f},
     {64, 128, 256, 4, 8, 1.20f},   {64, 128, 128, 4, 16, 1.10f},
 };
@@ -665,7 +706,7 @@ bool q16_ok(int k, const Params& p) {
   if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;
   if (p.d.kmask && f.bm != 64) return false;
   Band16 b;
-  return band16(p, f.bm, f.bn, f.nt, 3, f.bpc, b) >= 0;
+  return band16(p, f.bm, f.bn, f.nt, 4, f.bpc, b) >= 0;
 }
 
 double q16_cost(int k, const Params& p) {

@@ -42,6 +42,9 @@ LAYERS = {
     "r18_stem_7x7_b128": (3, 64, 7, 2, 3, 128, 224),
     "mbn_stem_3x3_b512": (3, 32, 3, 2, 1, 512, 224),
     "r50_1x1_1024_256_b256": (1024, 256, 1, 1, 0, 256, 14),
+    "r50_1x1_64_256_b256": (64, 256, 1, 1, 0, 256, 56),
+    "r50_1x1_s2_512_1024_b256": (512, 1024, 1, 2, 0, 256, 28),
+    "r18_1x1_s2_64_128_b128": (64, 128, 1, 2, 0, 128, 56),
 }
 
 
