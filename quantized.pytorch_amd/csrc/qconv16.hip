@@ -59,6 +59,14 @@ struct Band16 {
   int band_off, zero_off, tap_off, s_off, mask_off;
 };
 
+// s_waitcnt lgkmcnt(N) for hand-counted inline-asm LDS reads; the scheduling barrier keeps the
+// compiler from hoisting register-only MFMAs above it (cdna_hip_programming.md rule 18)
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ void wait_rt(int n) {
   if (n >= 24) wait_vmcnt<24>();
   else if (n >= 16) wait_vmcnt<16>();
@@ -203,7 +211,7 @@ __device__ __forceinline__ void epilogue16(const Params& p, const v4i (&acc)[C::
   }
 }
 
-template <class C, int EK, bool MASKED>
+template <class C, int EK, int NPL, bool MASKED>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv16_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Band16 b) {
   constexpr int BM = C::BM, BN = C::BN, W = C::W, TM = C::TM, TN = C::TN, D = C::D, NA = C::NA, NT = C::NT;
@@ -303,8 +311,10 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       bq16[j] = 16 * q;
     }
   }
-  const int tsub = b.npl == 4 ? 0 : (b.npl == 2 ? g >> 1 : g);  // which tap of a stage this lane's bytes hold
-  const int lpo = (g & (b.npl - 1)) * b.plane;                    // this lane's plane
+  static_assert(NPL == 1 || NPL == 2 || NPL == 4, "16-byte planes per band pixel");
+  static_assert(!MASKED || NPL == 1, "masked (space-to-depth) stems have 16-channel band pixels");
+  const int tsub = NPL == 4 ? 0 : (NPL == 2 ? g >> 1 : g);  // which tap of a stage this lane's bytes hold
+  const int lpo = (g & (NPL - 1)) * b.plane;                // this lane's plane
 
   // ---- weights: 16 rows x 64 B per DMA, slots XOR-swizzled by row bit 2 (source side)
   const int8_t* wblk = w + (int64_t)c0 * d.kpad;
@@ -325,7 +335,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     if (k < b.nbw) {
       const int piece = wave + W * k;
       int pl = piece / b.ppp;
-      pl = pl < b.npl ? pl : b.npl - 1;  // slack pieces past the last plane re-read valid bytes
+      pl = pl < NPL ? pl : NPL - 1;  // slack pieces past the last plane re-read valid bytes
       int q = (piece - (piece / b.ppp) * b.ppp) * 64 + lane;
       q = q < NBP ? q : NBP - 1;
       int gp;
@@ -348,7 +358,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   // ---- DMA issue
   auto issue_band = [&](int c, int bi) {
     int8_t* dst = smem + b.band_off + bi * b.bufsz;
-    const uint32_t co = (uint32_t)(c * 16 * b.npl);
+    const uint32_t co = (uint32_t)(c * 16 * NPL);
 #pragma unroll
     for (int k = 0; k < NBWMAX; ++k) {
       if (k < b.nbw) {
@@ -360,7 +370,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   };
   auto issue_w = [&](int c, int s, int slot) {
     if (QNN_ABLATE == 1) return;
-    const uint32_t ko = (uint32_t)(b.npl == 4 ? s * d.cp + 64 * c : 64 * s);
+    const uint32_t ko = (uint32_t)(NPL == 4 ? s * d.cp + 64 * c : 64 * s);
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       uint32_t off = aoff[j] + ko;
@@ -400,18 +410,31 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   // band offset (pixels) of stage s's tap for this lane's K bytes (uniform when npl == 4)
   auto tap_of = [&](int s) -> int {
     if (b.list) return 0;
-    int tt = s * b.tps + tsub;
+    int tt = NPL == 4 ? s : s * (4 / NPL) + tsub;
     if (tt >= p.taps) tt = 0;  // padded taps: any valid band bytes (their weights are 0, masked in sums)
     const int tr = (tt * p.kw_magic) >> 16, tc = tt - tr * d.kw;
     return tr * d.wp + (b.s2 ? (tc & 1) * b.we + (tc >> 1) : tc);
   };
+  // Fragment reads are inline asm: the compiler's waitcnt pass cannot see that the next
+  // stage's reads are younger than the registers the current MFMAs use (it waits
+  // lgkmcnt(0) there); the counts are kept by hand (lds_wait) instead.
   auto read_frags = [&](auto slotc, int bi, int s, v4i (&fa)[TM], v4i (&fb)[TN]) {
     constexpr int AO = decltype(slotc)::value * STAGE_A;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const v4i*>(smem + AO + offa + i * 1024);
+    for (int i = 0; i < TM; ++i)
+    {
+      v4i r;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(offa), "n"(AO + i * 1024));
+      fa[i] = r;
+    }
     const int base = b.band_off + bi * b.bufsz + lpo + 16 * tap_of(s);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const v4i*>(smem + base + bq16[j]);
+    for (int j = 0; j < TN; ++j) {
+      const int addr = base + bq16[j];
+      v4i r;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+      fb[j] = r;
+    }
   };
   auto mma = [&](const v4i (&fa)[TM], const v4i (&fb)[TN], int s) {
     if constexpr (MASKED) {
@@ -447,7 +470,8 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       const int q = tid + NT * u;
       if (q < NBP) {
         int sm = sacc[u];
-        for (int pl = 0; pl < b.npl; ++pl) {
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
           const v4i v = *reinterpret_cast<const v4i*>(bb + pl * b.plane + 16 * q);
           sm = __builtin_amdgcn_sdot4(v.x, ones, sm, false);
           sm = __builtin_amdgcn_sdot4(v.y, ones, sm, false);
@@ -480,6 +504,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   __builtin_amdgcn_s_barrier();
   if constexpr (!MASKED) band_sums(0);
   read_frags(std::integral_constant<int, 0>{}, 0, 0, fa0, fb0);
+  constexpr int NR = TM + TN < 15 ? TM + TN : 15;  // LDS reads of one stage's fragments (lgkmcnt <= 15)
   int s = 0;                                        // current stage's s
   int s1 = b.ns > 1 ? 1 : 0, bi1 = b.ns > 1 ? 0 : (b.nbuf > 1 ? 1 : 0);  // next stage's s and band buffer
   auto step = [&](auto slotc, int k) {
@@ -493,6 +518,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
         if (s1 == 0) band_sums(bi1);
       if constexpr ((SL & 1) == 0) read_frags(std::integral_constant<int, NX>{}, bi1, s1, fa1, fb1);
       else read_frags(std::integral_constant<int, NX>{}, bi1, s1, fa0, fb0);
+      lds_wait<NR>();  // this stage's fragments (read one step ago) landed; the next stage's may be in flight
+    } else {
+      lds_wait<0>();
     }
     if constexpr ((SL & 1) == 0) mma(fa0, fb0, s);
     else mma(fa1, fb1, s);
@@ -624,9 +652,9 @@ static int plan_lds(int lds_main, Params& q) {
   return lds > LDS_MAX ? -1 : lds;
 }
 
-template <class C, int EK, bool MASKED>
+template <class C, int EK, int NPL, bool MASKED>
 static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  auto kern = qconv16_kernel<C, EK, MASKED>;
+  auto kern = qconv16_kernel<C, EK, NPL, MASKED>;
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -643,11 +671,14 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
 
 template <class C, int EK>
 static int launch_m(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  if (p.d.kmask) {
-    if constexpr (C::BM == 64) return launch<C, EK, true>(x, w, p, s);
-    else return arg_error("tile configuration not built for this layer / epilogue kind");
+  const int npl = p.d.cp >= 64 ? 4 : p.d.cp / 16;
+  if (npl == 4 && !p.d.kmask) return launch<C, EK, 4, false>(x, w, p, s);
+  if constexpr (C::BM == 64) {  // few-channel inputs (stems, CIFAR): narrow output tiles only
+    if (p.d.kmask) return launch<C, EK, 1, true>(x, w, p, s);
+    if (npl == 2) return launch<C, EK, 2, false>(x, w, p, s);
+    if (npl == 1) return launch<C, EK, 1, false>(x, w, p, s);
   }
-  return launch<C, EK, false>(x, w, p, s);
+  return arg_error("tile configuration not built for this layer / epilogue kind");
 }
 
 template <class C>
@@ -704,7 +735,7 @@ bool q16_ok(int k, const Params& p) {
   if (k < 0 || k >= NQ) return false;
   const Info& f = INFO[k];
   if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;
-  if (p.d.kmask && f.bm != 64) return false;
+  if ((p.d.kmask || p.d.cp < 64) && f.bm != 64) return false;
   Band16 b;
   return band16(p, f.bm, f.bn, f.nt, 4, f.bpc, b) >= 0;
 }
