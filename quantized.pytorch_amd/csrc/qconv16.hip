@@ -39,12 +39,13 @@ struct Cfg {
   static constexpr int W = WGM * WGN, NT = 64 * W;
   static constexpr int BM = WGM * TM * 16, BN = WGN * TN * 16;
   static constexpr int STAGE_A = BM * 64;
-  static constexpr int NA = BM / 16 / W;  // weight DMA (16 rows x 64 B) per wave per stage
-  static_assert(BM % (16 * W) == 0, "weight DMA rows must split evenly over the waves");
+  static constexpr int AP = BM / 16;                 // weight DMA pieces (16 rows x 64 B) per stage
+  static constexpr int NA = AP >= W ? AP / W : 1;     // per wave (fewer pieces than waves: duplicated)
+  static_assert(AP % W == 0 || W % AP == 0, "weight DMA pieces must split evenly over the waves");
   static_assert(BM % 64 == 0, "epilogue staging moves 64-channel groups");
 };
 
-constexpr int NBWMAX = 8;  // band DMA pieces per wave per chunk
+constexpr int NBWMAX = 12;  // band DMA pieces per wave per chunk
 constexpr int PPTMAX = 4;  // band pixels per thread (channel sums)
 
 struct Band16 {
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   uint32_t aoff[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int row = 16 * (wave + W * j) + (lane >> 2);
+    const int row = 16 * ((wave + W * j) % C::AP) + (lane >> 2);
     const int crow = (c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0);
     aoff[j] = (uint32_t)(crow * d.kpad + 16 * ((lane & 3) ^ (((row >> 2) & 1) << 1)));
   }
@@ -375,8 +376,8 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     for (int j = 0; j < NA; ++j) {
       uint32_t off = aoff[j] + ko;
       asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(smem + slot * STAGE_A + (wave + W * j) * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(wblk + off),
+                                       (lds_ptr_t)(smem + slot * STAGE_A + ((wave + W * j) % C::AP) * 1024), 16, 0, 0);
     }
   };
   const int KT = b.kt;
@@ -490,51 +491,37 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     return n;
   };
 
-  // ---- software pipeline.  Stage k = (c, s) lives in weight slot k % D and its chunk's band
-  // buffer.  Its fragments are read one stage early (while stage k-1's MFMAs run), so the
-  // wait + barrier before that read covers stage k's DMA: at step k each wave waits for its
-  // own DMA of stage k+1 (issued D-2 steps earlier; stages k+2 .. k+D-2 stay in flight),
-  // passes the barrier, refills the slot of stage k-1 (read during step k-2) with stage
-  // k+D-1, reads stage k+1's fragments, then runs stage k's MFMAs.
-  static_assert(D == 4, "pipelined ring: 4 slots");
-  v4i fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  // ---- main loop.  Stage k = (c, s) lives in weight slot k % D and its chunk's band buffer.
+  // Before the barrier of stage k each wave waits for its own DMA of stage k (issued D-1
+  // stages earlier); stages k+1 .. k+D-2 stay in flight (weights, + the band chunk where
+  // one of them opens a chunk).  After the barrier the slot of stage k-1 is refilled with
+  // stage k+D-1.  Two waves per SIMD: one wave's LDS reads and DMA issue hide under its
+  // partner's MFMAs.
+  v4i fa[TM], fb[TN];
 #pragma unroll
   for (int k = 0; k < D - 1; ++k) issue_stage(k);
-  wait_rt(younger(0, 0, 1, D - 2));
-  __builtin_amdgcn_s_barrier();
-  if constexpr (!MASKED) band_sums(0);
-  read_frags(std::integral_constant<int, 0>{}, 0, 0, fa0, fb0);
-  constexpr int NR = TM + TN < 15 ? TM + TN : 15;  // LDS reads of one stage's fragments (lgkmcnt <= 15)
-  int s = 0;                                        // current stage's s
-  int s1 = b.ns > 1 ? 1 : 0, bi1 = b.ns > 1 ? 0 : (b.nbuf > 1 ? 1 : 0);  // next stage's s and band buffer
+  int s = 0, bi = 0;
   auto step = [&](auto slotc, int k) {
     constexpr int SL = decltype(slotc)::value;
-    constexpr int NX = (SL + 1) % D;
-    if (k + 1 < KT) {
-      wait_rt(younger(k, s, 2, D - 2));
-      __builtin_amdgcn_s_barrier();
-      issue_stage((SL + D - 1) % D);
-      if constexpr (!MASKED)
-        if (s1 == 0) band_sums(bi1);
-      if constexpr ((SL & 1) == 0) read_frags(std::integral_constant<int, NX>{}, bi1, s1, fa1, fb1);
-      else read_frags(std::integral_constant<int, NX>{}, bi1, s1, fa0, fb0);
-      lds_wait<NR>();  // this stage's fragments (read one step ago) landed; the next stage's may be in flight
-    } else {
-      lds_wait<0>();
-    }
-    if constexpr ((SL & 1) == 0) mma(fa0, fb0, s);
-    else mma(fa1, fb1, s);
-    s = s1;
-    if (++s1 == b.ns) {
-      s1 = 0;
-      if (++bi1 == b.nbuf) bi1 = 0;
+    wait_rt(younger(k, s, 1, D - 2));
+    __builtin_amdgcn_s_barrier();
+    issue_stage((SL + D - 1) % D);
+    if constexpr (!MASKED)
+      if (s == 0) band_sums(bi);
+    read_frags(slotc, bi, s, fa, fb);
+    lds_wait<0>();
+    mma(fa, fb, s);
+    if (++s == b.ns) {
+      s = 0;
+      if (++bi == b.nbuf) bi = 0;
     }
   };
   for (int k = 0; k < KT; k += D) {
     step(std::integral_constant<int, 0>{}, k);
     if (k + 1 < KT) step(std::integral_constant<int, 1>{}, k + 1);
     if (k + 2 < KT) step(std::integral_constant<int, 2>{}, k + 2);
-    if (k + 3 < KT) step(std::integral_constant<int, 3>{}, k + 3);
+    if constexpr (D == 4)
+      if (k + 3 < KT) step(std::integral_constant<int, 3>{}, k + 3);
   }
   wait_vmcnt<0>();  // the clamped tail DMAs still write LDS
 
@@ -622,8 +609,8 @@ static int band16(const Params& p, int BM, int BN, int nt, int D, int bpc, Band1
   b.nbw = (int)cdiv(npl * b.ppp, W);
   if (b.nbw > NBWMAX) return -1;
   b.bufsz = b.nbw * W * 1024;
-  b.nbuf = 2;  // a chunk's band is refilled D-1 stages before its first read: nbuf * ns > ns + D - 3
-  while (b.nbuf * b.ns <= b.ns + D - 3) ++b.nbuf;
+  b.nbuf = 2;  // a chunk's band lands D-1 stages before its first read: nbuf * ns >= ns + D - 1
+  while (b.nbuf * b.ns < b.ns + D - 1) ++b.nbuf;
   b.nbuf = std::min(b.nc, b.nbuf);
   b.band_off = D * BM * 64;
   b.zero_off = b.band_off + b.nbuf * b.bufsz;
@@ -693,32 +680,32 @@ static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStrea
   }
 }
 
-//   id   block (cout x px)   waves (each)          blocks/CU
-//   0    256 x 256           4 (64 x 256)          1   (one wave per SIMD: 512-register budget)
-//   1    256 x 208           4 (64 x 208)          1   (one 14x14 image + 12 px: 242 tiles for R50 l3)
+//   id   block (cout x px)   waves (each)          blocks/CU  (all: two waves per SIMD)
+//   0    256 x 256           8 (64 x 128)          1
+//   1    256 x 208           8 (32 x 208)          1   (a 14x14 image + 12 px: 242 tiles for R50 l3)
 //   2    128 x 256           8 (64 x 64)           1
 //   3    256 x 128           8 (64 x 64)           1
 //   4     64 x 256           4 (64 x 64)           2
 //   5    128 x 128           4 (64 x 64)           2
-//   6     64 x 128           4 (64 x 32)           4
-//   7     64 x 128           2 (64 x 64)           4
-using Q0 = Cfg<4, 1, 4, 16, 4, 1>;
-using Q1 = Cfg<4, 1, 4, 13, 4, 1>;
+//   6     64 x 128           4 (64 x 32)           2-4
+//   7     64 x 512           8 (64 x 64)           1   (64-channel layers: one weight stream per CU)
+using Q0 = Cfg<4, 2, 4, 8, 4, 1>;
+using Q1 = Cfg<8, 1, 2, 13, 4, 1>;
 using Q2 = Cfg<2, 4, 4, 4, 4, 1>;
 using Q3 = Cfg<4, 2, 4, 4, 4, 1>;
 using Q4 = Cfg<1, 4, 4, 4, 4, 2>;
 using Q5 = Cfg<2, 2, 4, 4, 4, 2>;
-using Q6 = Cfg<1, 4, 4, 2, 4, 4>;
-using Q7 = Cfg<1, 2, 4, 4, 4, 4>;
+using Q6 = Cfg<1, 4, 4, 2, 4, 2>;
+using Q7 = Cfg<1, 8, 4, 4, 4, 1>;
 constexpr int NQ = 8;
 struct Info {
   int bm, bn, nt, bpc, acc_tiles;
   float rate;
 };
 static const Info INFO[NQ] = {
-    {256, 256, 256, 1, 64, 2.00f}, {256, 208, 256, 1, 52, 1.95f}, {128, 256, 512, 1, 16, 1.75f},
+    {256, 256, 512, 1, 32, 2.00f}, {256, 208, 512, 1, 26, 1.95f}, {128, 256, 512, 1, 16, 1.75f},
     {256, 128, 512, 1, 16, 1.75f}, {64, 256, 256, 2, 16, 1.50f},  {128, 128, 256, 2, 16, 1.50f},
-    {64, 128, 256, 4, 8, 1.20f},   {64, 128, 128, 4, 16, 1.10f},
+    {64, 128, 256, 2, 8, 1.20f},   {64, 512, 512, 1, 16, 1.50f},
 };
 
 }  // namespace q16
@@ -734,7 +721,7 @@ bool q16_ok(int k, const Params& p) {
   using namespace q16;
   if (k < 0 || k >= NQ) return false;
   const Info& f = INFO[k];
-  if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;
+  if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;  // the general chain spills beside 128 acc regs
   if ((p.d.kmask || p.d.cp < 64) && f.bm != 64) return false;
   Band16 b;
   return band16(p, f.bm, f.bn, f.nt, 4, f.bpc, b) >= 0;

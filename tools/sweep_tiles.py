@@ -48,7 +48,7 @@ LAYERS = {
 }
 
 
-def sweep(name, shape, reps, dev):
+def sweep(name, shape, reps, dev, cfgs=None):
     cin, cout, k, st, pd, N, H = shape
     m = QConv2d(cin, cout, k, stride=st, padding=pd, bias=False, num_bits_grad=8, biprecision=True)
     wrap = nn.Sequential(m)
@@ -69,6 +69,8 @@ def sweep(name, shape, reps, dev):
     ref = None
     ops = 2 * N * cout * y.shape[2] * y.shape[3] * cin * k * k
     for t in range(_lib.CONV_TILES):
+        if cfgs is not None and t not in cfgs and t != 5:
+            continue
         d.tile = t + 1
         if not Engine._plan_ok(d, e):
             continue
@@ -103,6 +105,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--json")
+    ap.add_argument("--cfgs", nargs="*", type=int, help="only these configurations (and 5, the reference)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     _lib.load()
@@ -110,7 +113,7 @@ def main():
     for name, shape in LAYERS.items():
         if a.only and not any(o in name for o in a.only):
             continue
-        rows = sweep(name, shape, a.reps, dev)
+        rows = sweep(name, shape, a.reps, dev, a.cfgs)
         best = min(rows, key=lambda r: r["us"])
         for r in rows:
             line = json.dumps(r)
