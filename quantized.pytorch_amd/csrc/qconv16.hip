@@ -47,6 +47,7 @@ struct Cfg {
 
 constexpr int NBWMAX = 12;  // band DMA pieces per wave per chunk
 constexpr int PPTMAX = 4;  // band pixels per thread (channel sums)
+constexpr int NBS = 2;     // band DMA pieces per wave in every stage's DMA group
 
 struct Band16 {
   int list;            // 1: band pixel q = output pixel m0 + q (1x1); 0: padded input rows [R0, R1)
@@ -57,7 +58,7 @@ struct Band16 {
   int plane, ppp;      // LDS bytes per plane (multiple of 1 KiB), 1 KiB pieces per plane
   int nbw;             // band DMA pieces per wave per chunk (<= NBWMAX)
   int nbuf, bufsz;     // band buffers and their size
-  int band_off, zero_off, tap_off, s_off, mask_off;
+  int band_off, dummy_off, zero_off, tap_off, s_off, mask_off;
 };
 
 // s_waitcnt lgkmcnt(N) for hand-counted inline-asm LDS reads; the scheduling barrier keeps the
@@ -328,72 +329,53 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   }
   const int offa = (wm * 16 * TM + px) * 64 + 16 * (g ^ (((px >> 2) & 1) << 1));
 
-  // ---- band DMA sources of this lane's pieces (fixed across chunks; + 16*npl*c per chunk)
-  uint32_t bsrc[NBWMAX];
-#pragma unroll
-  for (int k = 0; k < NBWMAX; ++k) {
-    bsrc[k] = 0;
-    if (k < b.nbw) {
-      const int piece = wave + W * k;
-      int pl = piece / b.ppp;
-      pl = pl < NPL ? pl : NPL - 1;  // slack pieces past the last plane re-read valid bytes
-      int q = (piece - (piece / b.ppp) * b.ppp) * 64 + lane;
-      q = q < NBP ? q : NBP - 1;
-      int gp;
-      if (b.list) {
-        Pix P;
-        decode(m0 + q, P);
-        gp = (P.n * d.hp + P.ho * d.sh) * d.wp + P.wo * d.sw;
-      } else {
-        const int r = (int)__umulhi((uint32_t)q, b.wp_magic);
-        const int ci = q - r * d.wp;
-        const int col = b.s2 ? (ci < b.we ? 2 * ci : 2 * (ci - b.we) + 1) : ci;
-        gp = (R0 + r) * d.wp + col;
-      }
-      bsrc[k] = (uint32_t)(gp * d.cp + 16 * pl);
-    }
-  }
-
   if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
 
-  // ---- DMA issue
-  auto issue_band = [&](int c, int bi) {
-    int8_t* dst = smem + b.band_off + bi * b.bufsz;
-    const uint32_t co = (uint32_t)(c * 16 * NPL);
-#pragma unroll
-    for (int k = 0; k < NBWMAX; ++k) {
-      if (k < b.nbw) {
-        uint32_t off = bsrc[k] + co;
-        asm volatile("" : "+v"(off));
-        __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(dst + (wave + W * k) * 1024), 16, 0, 0);
-      }
-    }
+  // ---- DMA.  Band piece j of this wave = 1 KiB of the band buffer at piece (wave + W*j):
+  // plane pl, band pixels [64*(.), +64); its global source is recomputed on the fly.
+  auto band_src = [&](int j, int c) -> uint32_t {
+    const int id = wave + W * j;               // uniform
+    int pl = id / b.ppp;
+    const int qb = (id - pl * b.ppp) * 64;
+    pl = pl < NPL ? pl : NPL - 1;              // slack pieces past the last plane re-read valid bytes
+    int q = qb + lane;
+    q = q < NBP ? q : NBP - 1;
+    const int r = (int)__umulhi((uint32_t)q, b.wp_magic);
+    const int ci = q - r * d.wp;
+    const int col = b.s2 ? (ci < b.we ? 2 * ci : 2 * (ci - b.we) + 1) : ci;
+    return (uint32_t)(((R0 + r) * d.wp + col) * d.cp + 16 * pl + c * 16 * NPL);
   };
-  auto issue_w = [&](int c, int s, int slot) {
+  auto glds = [&](const int8_t* src, int8_t* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)dst, 16, 0, 0);
+  };
+  auto koff = [&](int c, int s) -> uint32_t { return (uint32_t)(NPL == 4 ? s * d.cp + 64 * c : 64 * s); };
+  const int KT = b.kt;
+  // DMA group of stage (c, s), issued D-1 stages ahead: its weights (NA pieces) and NBS band
+  // pieces -- slice s-(D-1) of chunk c+1 when c+1 < nc and s >= D-1, otherwise dummies (the
+  // input's zero page into this wave's scratch KiB, one L2 line).  Every group is exactly
+  // NA + NBS DMA per wave, so every wait below is a compile-time vmcnt.
+  auto issue_group = [&](int c, int s, int slot) {
     if (QNN_ABLATE == 1) return;
-    const uint32_t ko = (uint32_t)(NPL == 4 ? s * d.cp + 64 * c : 64 * s);
+    const uint32_t ko = koff(c, s);
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       uint32_t off = aoff[j] + ko;
       asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((const void*)(wblk + off),
-                                       (lds_ptr_t)(smem + slot * STAGE_A + ((wave + W * j) % C::AP) * 1024), 16, 0, 0);
+      glds(wblk + off, smem + slot * STAGE_A + ((wave + W * j) % C::AP) * 1024);
     }
-  };
-  const int KT = b.kt;
-  int ik = 0, ic = 0, is = 0, ib = 0;  // next stage to issue
-  auto issue_stage = [&](int slot) {
-    if (ik < KT) {
-      if (is == 0) issue_band(ic, ib);
-      issue_w(ic, is, slot);
-      if (++is == b.ns) {
-        is = 0, ++ic;
-        if (++ib == b.nbuf) ib = 0;
-      }
-    } else {
-      issue_w(b.nc - 1, b.ns - 1, slot);  // clamped: keeps every wave's DMA count uniform
+    const int cn = c + 1, bj0 = NBS * (s - (D - 1));
+    const bool slice = cn < b.nc && s >= D - 1;
+    int8_t* bdst = smem + b.band_off + (cn & 1) * b.bufsz;
+#pragma unroll
+    for (int u = 0; u < NBS; ++u) {
+      const int j = bj0 + u;
+      const bool real = slice && j < b.nbw;
+      uint32_t off = band_src(real ? j : 0, cn);
+      asm volatile("" : "+v"(off));
+      const int8_t* src = real ? x + off : x + d.zero_off;
+      int8_t* dst = real ? bdst + (wave + W * j) * 1024 : smem + b.dummy_off + wave * 1024;
+      glds(src, dst);
     }
-    ++ik;
   };
 
   v4i acc[TM][TN];
@@ -483,45 +465,52 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       }
     }
   };
-  // DMA groups younger than stage k's: stages k+1 .. k+n (weights, + band where one opens a chunk)
-  auto younger = [&](int k, int s, int from, int to) {
-    int n = 0;
+  // ---- main loop.  Stage k = (c, s) lives in weight slot k % D and band buffer c & 1.
+  // Before the barrier of stage k each wave waits for its own DMA group of stage k (issued
+  // D-1 stages earlier; the band chunk it reads was completed by older groups); the D-2
+  // younger groups stay in flight.  After the barrier the slot of stage k-1 is refilled
+  // with stage k+D-1's group.  Two waves per SIMD: one wave's LDS reads and DMA issue hide
+  // under its partner's MFMAs.  Branch-free apart from the chunk-start channel sums.
+  constexpr int YOUNG = (D - 2) * (NA + NBS);
+  {  // chunk 0's band, then the groups of stages 0 .. D-2 (clamped to the last stage)
 #pragma unroll
-    for (int dk = from; dk <= to; ++dk) n += NA + ((k + dk < KT && (s + dk) % b.ns == 0) ? b.nbw : 0);
-    return n;
-  };
-
-  // ---- main loop.  Stage k = (c, s) lives in weight slot k % D and its chunk's band buffer.
-  // Before the barrier of stage k each wave waits for its own DMA of stage k (issued D-1
-  // stages earlier); stages k+1 .. k+D-2 stay in flight (weights, + the band chunk where
-  // one of them opens a chunk).  After the barrier the slot of stage k-1 is refilled with
-  // stage k+D-1.  Two waves per SIMD: one wave's LDS reads and DMA issue hide under its
-  // partner's MFMAs.
+    for (int j = 0; j < NBWMAX; ++j) {
+      if (j < b.nbw) {
+        uint32_t off = band_src(j, 0);
+        asm volatile("" : "+v"(off));
+        glds(x + off, smem + b.band_off + (wave + W * j) * 1024);
+      }
+    }
+  }
+  int ca = 0, sa = 0;  // the newest issued group's stage
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) {
+    issue_group(ca, sa, k);
+    if (k + 1 < D - 1 && ca * b.ns + sa + 1 < KT)
+      if (++sa == b.ns) sa = 0, ++ca;
+  }
   v4i fa[TM], fb[TN];
-#pragma unroll
-  for (int k = 0; k < D - 1; ++k) issue_stage(k);
   int s = 0, bi = 0;
-  auto step = [&](auto slotc, int k) {
+  auto step = [&](auto slotc) {
     constexpr int SL = decltype(slotc)::value;
-    wait_rt(younger(k, s, 1, D - 2));
+    wait_vmcnt<YOUNG>();
     __builtin_amdgcn_s_barrier();
-    issue_stage((SL + D - 1) % D);
+    if (ca * b.ns + sa + 1 < KT)
+      if (++sa == b.ns) sa = 0, ++ca;
+    issue_group(ca, sa, (SL + D - 1) % D);
     if constexpr (!MASKED)
       if (s == 0) band_sums(bi);
     read_frags(slotc, bi, s, fa, fb);
     lds_wait<0>();
     mma(fa, fb, s);
-    if (++s == b.ns) {
-      s = 0;
-      if (++bi == b.nbuf) bi = 0;
-    }
+    if (++s == b.ns) s = 0, bi ^= 1;
   };
   for (int k = 0; k < KT; k += D) {
-    step(std::integral_constant<int, 0>{}, k);
-    if (k + 1 < KT) step(std::integral_constant<int, 1>{}, k + 1);
-    if (k + 2 < KT) step(std::integral_constant<int, 2>{}, k + 2);
+    step(std::integral_constant<int, 0>{});
+    if (k + 1 < KT) step(std::integral_constant<int, 1>{});
+    if (k + 2 < KT) step(std::integral_constant<int, 2>{});
     if constexpr (D == 4)
-      if (k + 3 < KT) step(std::integral_constant<int, 3>{}, k + 3);
+      if (k + 3 < KT) step(std::integral_constant<int, 3>{});
   }
   wait_vmcnt<0>();  // the clamped tail DMAs still write LDS
 
@@ -591,6 +580,7 @@ static int band16(const Params& p, int BM, int BN, int nt, int D, int bpc, Band1
   b.kt = b.nc * b.ns;
   if ((npl < 4 ? b.ns * 64 : p.taps * d.cp) > d.kpad) return -1;
   b.list = p.taps == 1;
+  if (b.list) return -1;  // 1x1: qconv.hip's ring kernels (no im2col re-reads to save)
   b.s2 = !b.list && d.sh == 2;
   b.we = (d.wp + 1) / 2;
   b.wp_magic = (uint32_t)((0x100000000ULL + (uint64_t)d.wp - 1) / (uint64_t)d.wp);
@@ -609,11 +599,12 @@ static int band16(const Params& p, int BM, int BN, int nt, int D, int bpc, Band1
   b.nbw = (int)cdiv(npl * b.ppp, W);
   if (b.nbw > NBWMAX) return -1;
   b.bufsz = b.nbw * W * 1024;
-  b.nbuf = 2;  // a chunk's band lands D-1 stages before its first read: nbuf * ns >= ns + D - 1
-  while (b.nbuf * b.ns < b.ns + D - 1) ++b.nbuf;
-  b.nbuf = std::min(b.nc, b.nbuf);
+  // chunk c+1's band is issued in NBS-piece slices with the DMA groups of stages (c, D-1 .. ns-1)
+  if (b.nc > 1 && b.nbw > NBS * (b.ns - D + 1)) return -1;
+  b.nbuf = b.nc > 1 ? 2 : 1;
   b.band_off = D * BM * 64;
-  b.zero_off = b.band_off + b.nbuf * b.bufsz;
+  b.dummy_off = b.band_off + b.nbuf * b.bufsz;
+  b.zero_off = b.dummy_off + W * 1024;
   b.tap_off = b.zero_off + 64;
   b.s_off = b.tap_off + 256;
   b.mask_off = b.s_off + (int)nbp * 4;
