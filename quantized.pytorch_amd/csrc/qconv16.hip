@@ -694,9 +694,9 @@ struct Info {
   float rate;
 };
 static const Info INFO[NQ] = {
-    {256, 256, 512, 1, 32, 2.00f}, {256, 208, 512, 1, 26, 1.95f}, {128, 256, 512, 1, 16, 1.75f},
-    {256, 128, 512, 1, 16, 1.75f}, {64, 256, 256, 2, 16, 1.50f},  {128, 128, 256, 2, 16, 1.50f},
-    {64, 128, 256, 2, 8, 1.20f},   {64, 512, 512, 1, 16, 1.50f},
+    {256, 256, 512, 1, 32, 0.74f}, {256, 208, 512, 1, 26, 0.70f}, {128, 256, 512, 1, 16, 0.55f},
+    {256, 128, 512, 1, 16, 0.55f}, {64, 256, 256, 2, 16, 0.55f},  {128, 128, 256, 2, 16, 0.55f},
+    {64, 128, 256, 2, 8, 0.45f},   {64, 512, 512, 1, 16, 0.50f},
 };
 
 }  // namespace q16
