@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 5
+#define QNN_ABI_VERSION 6
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -150,6 +150,23 @@ typedef struct qnn_conv_desc {
  *   index(m, c) = (((m/32)*CT + c/32)*4 + (c%32)/8)*256 + (m%32 + 32*((c/4)%2))*4 + c%4
  * with CT = ceil(cout/32); a map holds ceil(M/32)*32 * CT*32 floats.  Producer and
  * consumer of a residual agree on it (qnn_maxpool_bn, qnn_avgpool_quant take it too). */
+/* One link of a residual code chain (qnn_epilogue.res): the RangeBN input codes a producer
+ * wrote (its out_bncode, byte C-tile layout) and that RangeBN's eval parameters, so a
+ * consumer recomputes the producer's fp32 value op for op:
+ *   g(q) = fl(fl(fl(fl(q*scale) + min) - mean[c]) * sq[c]) * wq[c]) + bq[c]   (quantize.py:488-499)
+ * Byte C-tile layout of a [m][cout] code map (the MFMA accumulator image, 1 byte per value):
+ *   index(m, c) = (((m/32)*CT + c/32)*64 + m%32 + 32*((c/4)%2))*16 + 4*((c%32)/8) + c%4
+ * so a wave reads / writes a 32x32 sub-tile as one coalesced 16-byte access per lane. */
+typedef struct qnn_res_link {
+  const uint8_t* code;
+  const float* mean;
+  const float* sq;
+  const float* wq;
+  const float* bq;
+  float min, scale;
+} qnn_res_link;
+#define QNN_MAX_RES 4
+
 typedef struct qnn_epilogue {
   int mode;
   const float* sxsw;
@@ -178,6 +195,18 @@ typedef struct qnn_epilogue {
                          whole RangeBN -> ReLU -> consumer-quantizer chain tabulated per
                          channel (qnn_bn_code_lut); needs bn, out_code0 only, no residual */
   int f32_tiled;      /* mode 1: residual and out_f32 in the C-tile layout (else NHWC)     */
+  /* Residual as a code chain (mode 1, resnet_quantized.py:60-68 / :105-113): instead of
+   * reading an fp32 block input, recompute it from 1-byte codes (res[], qnn_res_link):
+   *   r = residual ? residual (fp32)                                   (links 0 .. nres-1)
+   *                : (res_relu0 ? max(g_0(q_0), 0) : g_0(q_0))         (links 1 .. nres-1)
+   *   r = max(g_l(q_l) + r, 0)   for each remaining link l            (a block's output)
+   * the first form continues a chain from an fp32 checkpoint, the second starts it from a
+   * downsample branch's RangeBN codes (res_relu0 = 0) or the stem max-pool's (= 1).  The
+   * result is bitwise the fp32 map the producers would have stored.  0 <= nres <= 4. */
+  int nres;
+  int res_relu0;
+  qnn_res_link res[QNN_MAX_RES];
+  int bncode_tiled;   /* out_bncode in the byte C-tile layout (a chain link), else NHWC uint8 */
 } qnn_epilogue;
 
 /* Eval forward of QConv2d / QLinear (quantize.py:314-349, :398-428; biprecision's
@@ -249,11 +278,13 @@ int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out
  * (uint8, the stem conv's out_bncode).  g_c = [relu o] RangeBN_eval is monotone in the
  * code (non-increasing where sq*wq < 0), so max over the window of g_c(q_i) = g_c(max q_i)
  * (min where decreasing); padding positions are skipped (-inf).  Outputs: out_f32 =
- * g_c(q*) (fp32 [m][c], NHWC or C-tile by f32_tiled; nullable) and codes lut{0,1}[c][q*]
- * (qnn_bn_code_lut) into consumer buffers code{0,1} (nullable).  c % 16 == 0. */
+ * g_c(q*) (fp32 [m][c], NHWC or C-tile by f32_tiled; nullable), out_code = q* itself (the
+ * byte C-tile layout of qnn_res_link: a residual chain start with res_relu0 = relu;
+ * nullable) and codes lut{0,1}[c][q*] (qnn_bn_code_lut) into consumer buffers code{0,1}
+ * (nullable).  c % 16 == 0. */
 int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
-                   const qnn_bn_params* bn, int relu, float* out_f32, int f32_tiled, const int8_t* lut0,
-                   const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                   const qnn_bn_params* bn, int relu, float* out_f32, int f32_tiled, uint8_t* out_code,
+                   const int8_t* lut0, const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
                    qnn_stream_t stream);
 
 /* Depthwise QConv2d (groups == c, mobilenet_quantized.py:38-40) fused with its RangeBN and

@@ -6,7 +6,7 @@
 
 #include <algorithm>
 
-#include "qnn_internal.h"
+#include "qconv_common.h"
 
 namespace qnn {
 
@@ -53,6 +53,7 @@ __device__ __forceinline__ uint32_t max_u8x4(uint32_t a, uint32_t b) {
 __global__ __launch_bounds__(256) void maxpool_bn_kernel(const uint8_t* __restrict__ q, int n, int h, int w, int c,
                                                          int k, int stride, int pad, int ho, int wo,
                                                          qnn_bn_params bn, int relu, float* out_f32, int tiled,
+                                                         uint8_t* __restrict__ out_code,
                                                          const int8_t* __restrict__ lut0, qnn_code_out c0,
                                                          const int8_t* __restrict__ lut1, qnn_code_out c1) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -104,6 +105,14 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const uint8_t* __restri
       }
     }
     const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
+    if (out_code) {  // the pooled RangeBN input codes: a residual chain start (byte C-tile)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int ch = cb + 4 * s4;
+        *reinterpret_cast<uint32_t*>(out_code + btile_off((int)(m >> 5), ch >> 5, ct, (int)(m & 31) + 32 * ((ch >> 2) & 1)) +
+                                     4 * ((ch & 31) >> 3)) = qd[s4];
+      }
+    }
     if (out_f32) {
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
@@ -380,8 +389,8 @@ using namespace qnn;
 extern "C" {
 
 int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stride, int pad, int ho, int wo,
-                   const qnn_bn_params* bn, int relu, float* out_f32, int f32_tiled, const int8_t* lut0,
-                   const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                   const qnn_bn_params* bn, int relu, float* out_f32, int f32_tiled, uint8_t* out_code,
+                   const int8_t* lut0, const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
                    qnn_stream_t stream) {
   QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && c > 0 && c % 16 == 0 && c <= 256 && k > 0 && stride > 0 && pad >= 0 &&
                   2 * pad <= k,
@@ -391,7 +400,8 @@ int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stri
   const bool has0 = code0 && code0->ptr, has1 = code1 && code1->ptr;
   QNN_REQUIRE(!has0 || (lut0 && (((uintptr_t)lut0) & 15) == 0), "code0 needs a 16-B aligned lut0");
   QNN_REQUIRE(!has1 || (lut1 && (((uintptr_t)lut1) & 15) == 0), "code1 needs a 16-B aligned lut1");
-  QNN_REQUIRE(out_f32 || has0 || has1, "no output");
+  QNN_REQUIRE(out_f32 || out_code || has0 || has1, "no output");
+  QNN_REQUIRE(!out_code || (((uintptr_t)out_code) & 15) == 0, "out_code must be 16-byte aligned");
   QNN_REQUIRE(!out_f32 || (((uintptr_t)out_f32) & 15) == 0, "out_f32 must be 16-byte aligned");
   auto code16 = [&](const qnn_code_out* o) {
     return !o || !o->ptr || (o->cp >= c && o->cp % 16 == 0 && o->scale > 0.f && o->pad >= 0 &&
@@ -408,7 +418,7 @@ int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stri
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(maxpool_bn)");
   const int64_t threads = cdiv((int64_t)n * ho * wo, 32) * (c / 16) * 32;
   hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(threads)), dim3(256), lds, (hipStream_t)stream, q, n, h, w, c,
-                     k, stride, pad, ho, wo, *bn, relu, out_f32, f32_tiled, has0 ? lut0 : nullptr, c0,
+                     k, stride, pad, ho, wo, *bn, relu, out_f32, f32_tiled, out_code, has0 ? lut0 : nullptr, c0,
                      has1 ? lut1 : nullptr, c1);
   QNN_LAUNCH_CHECK("qnn_maxpool_bn");
   return QNN_OK;

@@ -252,7 +252,48 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
     const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
     const CodeDst tb = {reinterpret_cast<int8_t*>(e.out_bncode), d.cout, 0, d.ho, d.wo};
     const bool has_res = EK == EK_GEN && e.residual != nullptr;
-    // residual of sub-tile (i, j): 4 float4 per lane, fetched one sub-tile ahead
+    const int nres = EK == EK_GEN ? e.nres : 0;
+    const bool want_bn = EK == EK_BNCODE || (EK == EK_GEN && e.out_bncode);
+    // residual code chain (qnn_res_link): one 16-byte byte-C-tile load per link per sub-tile
+    const float* s_chain = s_f + (7 + e.nclass) * BM;
+    auto load_chain = [&](v4i (&rc)[QNN_MAX_RES], int i, int j) {
+      int mt = (m0 + wn * 32 * TN + j * 32) >> 5;
+      mt = mt < (p.M + 31) >> 5 ? mt : ((p.M + 31) >> 5) - 1;  // the map holds ceil(M/32) pixel tiles
+      int ctb = (c0 + wm * 32 * TM + i * 32) >> 5;
+      ctb = ctb < p.ct ? ctb : p.ct - 1;  // channel tiles past cout: any in-bounds bytes (unused)
+      const int64_t off = btile_off(mt, ctb, p.ct, lane);
+#pragma unroll
+      for (int l = 0; l < QNN_MAX_RES; ++l)
+        if (l < nres) rc[l] = *reinterpret_cast<const v4i*>(e.res[l].code + off);
+    };
+    // g_l(q) for the 4 channels cl..cl+3 of register group g (quantize.py:488-499 op order)
+    auto link = [&](const v4i (&rc)[QNN_MAX_RES], int l, int g, int cl, f2 (&o)[2]) {
+      const unsigned wd = (unsigned)rc[l][g];
+      const float* sp = s_chain + 4 * l * BM + cl;
+      const float4 mn4 = *reinterpret_cast<const float4*>(sp);
+      const float4 sq4 = *reinterpret_cast<const float4*>(sp + BM);
+      const float4 wq4 = *reinterpret_cast<const float4*>(sp + 2 * BM);
+      const float4 bq4 = *reinterpret_cast<const float4*>(sp + 3 * BM);
+      const f2 s2 = {e.res[l].scale, e.res[l].scale}, m2 = {e.res[l].min, e.res[l].min};
+      const f2 q[2] = {{(float)(wd & 255u), (float)((wd >> 8) & 255u)},
+                       {(float)((wd >> 16) & 255u), (float)(wd >> 24)}};
+      const f2 mn[2] = {{mn4.x, mn4.y}, {mn4.z, mn4.w}}, sq[2] = {{sq4.x, sq4.y}, {sq4.z, sq4.w}};
+      const f2 wq[2] = {{wq4.x, wq4.y}, {wq4.z, wq4.w}}, bq[2] = {{bq4.x, bq4.y}, {bq4.z, bq4.w}};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f2 t = q[h] * s2;
+        t = t + m2;
+        t = t - mn[h];
+        t = t * sq[h];
+        t = t * wq[h];
+        o[h] = t + bq[h];
+      }
+    };
+    // fetched one sub-tile ahead, except under the 128-VGPR budget of 4 blocks per CU
+    constexpr bool CAHEAD = C::BPC < 4;
+    v4i ccur[QNN_MAX_RES], cnxt[CAHEAD ? QNN_MAX_RES : 1][QNN_MAX_RES];
+    if (CAHEAD && EK == EK_GEN && nres > 0) load_chain(ccur, 0, 0);
+    // fp32 residual of sub-tile (i, j): 4 float4 per lane
     auto load_res = [&](float4 (&r)[4], int i, int j) {
       const int m = pm[j] < p.M ? pm[j] : p.M - 1;
 #pragma unroll
@@ -263,19 +304,23 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
         r[g] = *reinterpret_cast<const float4*>(e.residual + fi);
       }
     };
-    float4 rcur[4], rnxt[4];
-    if (EK == EK_GEN && has_res) load_res(rcur, 0, 0);
+    float4 rcur[4];  // fp32 residual (a chain checkpoint): loaded per sub-tile
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int cb = c0 + wm * 32 * TM + i * 32;  // first channel of this lane's 32-channel group
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if (EK == EK_GEN && has_res) {
-          if (j + 1 < TN) load_res(rnxt, i, j + 1);
-          else if (i + 1 < TM) load_res(rnxt, i + 1, 0);
+        if (EK == EK_GEN && has_res) load_res(rcur, i, j);
+        if (EK == EK_GEN && nres > 0) {
+          if constexpr (CAHEAD) {
+            if (j + 1 < TN) load_chain(cnxt[0], i, j + 1);
+            else if (i + 1 < TM) load_chain(cnxt[0], i + 1, 0);
+          } else {
+            load_chain(ccur, i, j);
+          }
         }
         const bool pok = pm[j] < p.M;
-        int k0[4], k1[4];
+        int k0[4], k1[4], kb[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int cl = cb - c0 + 8 * g + 4 * fh;  // local channel of reg 4g (+u)
@@ -299,8 +344,9 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
             qb[0] = qclamp2(v[0], bnp);
             qb[1] = qclamp2(v[1], bnp);
           }
+          kb[g] = 0;
+          if (want_bn && cok) kb[g] = pack4(qb[0] + MAGIC_U8, qb[1] + MAGIC_U8);
           if constexpr (EK == EK_BNCODE) {
-            k0[g] = cok ? pack4(qb[0] + MAGIC_U8, qb[1] + MAGIC_U8) : 0;
             continue;
           } else {
             if (e.bn_mean) {
@@ -320,10 +366,36 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
                 v[h] = o + bq[h];             // + q(bias)
               }
             }
-            if (has_res) {
-              const float4 r4 = rcur[g];
-              v[0] = v[0] + (f2){r4.x, r4.y};
-              v[1] = v[1] + (f2){r4.z, r4.w};
+            if (has_res || nres > 0) {
+              // the block input: fp32, or recomputed from the chain exactly as its producers did
+              f2 r[2];
+              int l0 = 0;
+              if (has_res) {
+                const float4 r4 = rcur[g];
+                r[0] = (f2){r4.x, r4.y};
+                r[1] = (f2){r4.z, r4.w};
+              } else {
+                link(ccur, 0, g, cl, r);
+                if (e.res_relu0) {
+                  r[0].x = fmaxf(r[0].x, 0.f); r[0].y = fmaxf(r[0].y, 0.f);
+                  r[1].x = fmaxf(r[1].x, 0.f); r[1].y = fmaxf(r[1].y, 0.f);
+                }
+                l0 = 1;
+              }
+#pragma unroll
+              for (int l = 0; l < QNN_MAX_RES; ++l) {
+                if (l < l0 || l >= nres) continue;
+                f2 o[2];
+                link(ccur, l, g, cl, o);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                  const f2 t = o[h] + r[h];
+                  r[h].x = fmaxf(t.x, 0.f);
+                  r[h].y = fmaxf(t.y, 0.f);
+                }
+              }
+              v[0] = v[0] + r[0];
+              v[1] = v[1] + r[1];
             }
             if (e.relu) {
               v[0].x = fmaxf(v[0].x, 0.f); v[0].y = fmaxf(v[0].y, 0.f);
@@ -340,17 +412,25 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
           }
         }
         const int ch = cb + 16 * fh;
+        if (want_bn) {
+          if (e.bncode_tiled) {  // chain link: lane-linear 16 bytes of the sub-tile
+            if (cb < d.cout && m0 + wn * 32 * TN + j * 32 < p.M)  // sub-tiles inside the ceil(M/32)*32 map
+              *reinterpret_cast<v4i*>(e.out_bncode + btile_off((m0 + wn * 32 * TN + j * 32) >> 5, cb >> 5, p.ct, lane)) =
+                  (v4i){kb[0], kb[1], kb[2], kb[3]};
+          } else {
+            store_codes(tb, pn[j], pho[j], pwo[j], ch, pok, gather16(kb[0], kb[1], kb[2], kb[3]));
+          }
+        }
         if constexpr (EK == EK_BNCODE) {
-          store_codes(tb, pn[j], pho[j], pwo[j], ch, pok, gather16(k0[0], k0[1], k0[2], k0[3]));
         } else {
           if (EK == EK_LUT || e.out_code0)
             store_codes(t0, pn[j], pho[j], pwo[j], ch, pok, gather16(k0[0], k0[1], k0[2], k0[3]));
           if (EK == EK_GEN && e.out_code1)
             store_codes(t1, pn[j], pho[j], pwo[j], ch, pok, gather16(k1[0], k1[1], k1[2], k1[3]));
         }
-        if (EK == EK_GEN && has_res) {
+        if (CAHEAD && EK == EK_GEN && nres > 0) {
 #pragma unroll
-          for (int g = 0; g < 4; ++g) rcur[g] = rnxt[g];
+          for (int l = 0; l < QNN_MAX_RES; ++l) ccur[l] = cnxt[0][l];
         }
       }
     }
@@ -1190,7 +1270,8 @@ template <class C>
 static int plan_epi_lds(int lds_main, Params& q) {
   lds_main = (lds_main + 15) & ~15;
   const int k = epi_kind(q.e);
-  const int epi = 4 * (7 + q.e.nclass) * C::BM + (k == EK_LUT ? 256 * C::BM : 0);
+  const int epi = 4 * (7 + q.e.nclass) * C::BM + (k == EK_LUT ? 256 * C::BM : 0) +
+                  (k == EK_GEN ? 16 * q.e.nres * C::BM : 0);
   const int scr = k == EK_NCHW ? 4096 * C::W : 0;
   int lds;
   if (lds_main + epi <= LDS_MAX / C::BPC && scr <= lds_main) {
@@ -1534,6 +1615,14 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
                 "lut needs RangeBN, exactly one code output, no residual/fp32/bncode, 16-B aligned");
     QNN_REQUIRE(!e.f32_tiled || ((((uintptr_t)e.out_f32) & 15) == 0 && (((uintptr_t)e.residual) & 15) == 0),
                 "C-tile fp32 maps must be 16-byte aligned");
+    QNN_REQUIRE(e.nres >= 0 && e.nres <= QNN_MAX_RES && (e.nres == 0 || (!e.lut && e.bn_mean)) &&
+                    (!e.res_relu0 || (e.nres > 0 && !e.residual)),
+                "residual chain: 0..4 links, needs RangeBN, no lut; res_relu0 only for a code-started chain");
+    for (int l = 0; l < e.nres; ++l) {
+      const qnn_res_link& r = e.res[l];
+      QNN_REQUIRE(r.code && (((uintptr_t)r.code) & 15) == 0 && r.mean && r.sq && r.wq && r.bq && r.scale > 0.f,
+                  "bad residual chain link (16-B aligned codes, RangeBN params, scale > 0)");
+    }
   }
   hipStream_t s = (hipStream_t)stream;
   const int k = pick_cfg(p);

@@ -713,6 +713,7 @@ bool q16_ok(int k, const Params& p) {
   if (k < 0 || k >= NQ) return false;
   const Info& f = INFO[k];
   if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;  // the general chain spills beside 128 acc regs
+  if (p.e.nres > 0 || (p.e.out_bncode && p.e.bncode_tiled)) return false;  // residual code chains: qconv.hip only
   if ((p.d.kmask || p.d.cp < 64) && f.bm != 64) return false;
   Band16 b;
   return band16(p, f.bm, f.bn, f.nt, 4, f.bpc, b) >= 0;

@@ -66,9 +66,16 @@ static inline int epi_kind(const qnn_epilogue& e) {
   return EK_GEN;
 }
 
+// Byte offset of lane `lane`'s 16 bytes of the 32x32 sub-tile (pixel tile mt, channel tile
+// ctb) of a byte C-tile code map (include/qnn.h, qnn_res_link): lane-linear 1 KiB blocks.
+__device__ __forceinline__ int64_t btile_off(int mt, int ctb, int ct, int lane) {
+  return (((int64_t)mt * ct + ctb) * 64 + lane) * 16;
+}
+
 // Epilogue data in LDS at p.epi_off (f32 unless noted):
 //   [0,BM) sxsw  [BM,2BM) sxbw  [2BM,3BM) bias  [3BM..7BM) bn mean/sq/wq/bq
-//   [7BM, (7+nclass)BM) border table [cls][BM]  then (EK_LUT) int8 LUT [BM][256]
+//   [7BM, (7+nclass)BM) border table [cls][BM]  then (EK_LUT) int8 LUT [BM][256], or
+//   (EK_GEN, residual code chain) [nres][mean/sq/wq/bq][BM] of the chain links
 // moved by LDS-DMA (4 bytes per lane for the vectors and the table, 16 for the LUT), one
 // job per wave-instruction, so the whole staging is ~8 DMA per wave and one round trip.
 // Channels past cout read channel cout-1 (their outputs are never stored).
@@ -78,7 +85,7 @@ __device__ __forceinline__ void stage_epi(const Params& p, const int8_t* x, int8
   const qnn_epilogue& e = p.e;
   const int cmax = p.d.cout - 1;
   const int nvec = (EK != EK_NCHW && e.bn_mean) ? 7 : 3;
-  const int nf = (nvec + e.nclass) * CH;
+  const int nf = (nvec + e.nclass + (EK == EK_GEN ? 4 * e.nres : 0)) * CH;
   for (int jb = wave; jb < nf; jb += W) {
     const int v = jb / CH, k = jb - v * CH;
     const int arr = v < nvec ? v : 7 + (v - nvec);
@@ -100,7 +107,15 @@ __device__ __forceinline__ void stage_epi(const Params& p, const int8_t* x, int8
       case 4: src = e.bn_sq; break;
       case 5: src = e.bn_wq; break;
       case 6: src = e.bn_bq; break;
-      default: src = e.table + (int64_t)(arr - 7) * p.d.cout; break;
+      default:
+        if (arr - 7 < e.nclass) {
+          src = e.table + (int64_t)(arr - 7) * p.d.cout;
+        } else {  // chain link l, vector k (mean, sq, wq, bq)
+          const int lk = arr - 7 - e.nclass, l = lk >> 2, k = lk & 3;
+          const qnn_res_link& r = e.res[l];
+          src = k == 0 ? r.mean : k == 1 ? r.sq : k == 2 ? r.wq : r.bq;
+        }
+        break;
     }
     __builtin_amdgcn_global_load_lds((const void*)(src + c), (lds_ptr_t)(dst + 4 * (arr * BM + 64 * k)), 4, 0, 0);
   }

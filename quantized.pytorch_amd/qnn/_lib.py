@@ -16,7 +16,7 @@ import torch  # noqa: F401  (binds the process HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 CONV_TILES = 26  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
@@ -26,6 +26,15 @@ class ConvDesc(ctypes.Structure):
     """qnn_conv_desc (include/qnn.h)."""
     _fields_ = [(n, c_int) for n in ("n", "hp", "wp", "cp", "zero_off", "cout", "cout_pad", "kh", "kw", "sh", "sw",
                                      "ho", "wo", "kpad")] + [("kmask", c_ptr), ("tile", c_int)]
+
+
+class ResLink(ctypes.Structure):
+    """qnn_res_link (include/qnn.h)."""
+    _fields_ = [("code", c_ptr), ("mean", c_ptr), ("sq", c_ptr), ("wq", c_ptr), ("bq", c_ptr), ("min", c_float),
+                ("scale", c_float)]
+
+
+MAX_RES = 4  # QNN_MAX_RES
 
 
 class Epilogue(ctypes.Structure):
@@ -39,7 +48,8 @@ class Epilogue(ctypes.Structure):
                 ("code0_wp", c_int), ("code0_neg_min", c_float), ("code0_scale", c_float), ("code0_qmax", c_float),
                 ("out_code1", c_ptr), ("code1_cp", c_int), ("code1_pad", c_int), ("code1_hp", c_int),
                 ("code1_wp", c_int), ("code1_neg_min", c_float), ("code1_scale", c_float), ("code1_qmax", c_float),
-                ("lut", c_ptr), ("f32_tiled", c_int)]
+                ("lut", c_ptr), ("f32_tiled", c_int), ("nres", c_int), ("res_relu0", c_int),
+                ("res", ResLink * MAX_RES), ("bncode_tiled", c_int)]
 
 class BnParams(ctypes.Structure):
     """qnn_bn_params (include/qnn.h)."""
@@ -72,7 +82,7 @@ SIGNATURES = {
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
     "qnn_maxpool_bn": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,
-                       c_int, c_ptr, _PC, c_ptr, _PC, c_ptr],
+                       c_int, c_ptr, c_ptr, _PC, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],

@@ -63,6 +63,9 @@ class _Act:
         self.H, self.W, self.C = H, W, C
         self.codes = {}   # consumer module -> (buffer, CodeOut)
         self.f32 = None   # fp32 [N*H*W][C] in the C-tile layout
+        # how a residual consumer recomputes this fp32 value (qnn_epilogue.residual/res):
+        # (fp32 checkpoint or None, [(byte C-tile RangeBN code map, RangeBN)], relu of link 0)
+        self.res = None
 
 
 class Engine:
@@ -144,6 +147,12 @@ class Engine:
         self.keep.append(t)
         return t
 
+    def _btiled(self, H, W, C):
+        """A byte C-tile code map (qnn_res_link.code) for an [N*H*W][C] activation."""
+        t = torch.empty(ctile_numel(self.N * H * W, C), dtype=torch.uint8, device=self.dev)
+        self.keep.append(t)
+        return t
+
     def _f32_for(self, act):
         if act.f32 is None:
             act.f32 = self._tiled(act.H, act.W, act.C)
@@ -184,10 +193,12 @@ class Engine:
         self.ops.append(fn)
         self.launch_names.append(name)
 
-    def _conv(self, conv, src, H, W, bn=None, residual=None, relu=False, outs=(), out_f32=None, out_bncode=None,
-              mode=1, logits=None):
+    def _conv(self, conv, src, H, W, bn=None, chain=None, relu=False, outs=(), out_f32=None, out_bncode=None,
+              bncode_tiled=False, mode=1, logits=None):
         """One fused contraction.  src: (buf, CodeOut, geom) of conv's input codes, or a
-        ('s2d', buf, geom) tuple for a space-to-depth stem."""
+        ('s2d', buf, geom) tuple for a space-to-depth stem.  chain: the residual added
+        after RangeBN (an _Act.res); out_bncode: RangeBN's input codes (byte C-tile when
+        bncode_tiled: a chain link)."""
         kh, kw = conv.kernel_size if isinstance(conv, QConv2d) else (1, 1)
         sh, sw = conv.stride if isinstance(conv, QConv2d) else (1, 1)
         ph, pw = conv.padding if isinstance(conv, QConv2d) else (0, 0)
@@ -224,7 +235,15 @@ class Engine:
                 b = self._bn(bn)
                 e.bn_mean, e.bn_sq, e.bn_wq, e.bn_bq = b.mean, b.sq, b.wq, b.bq
                 e.bn_neg_min, e.bn_min, e.bn_scale, e.bn_qmax = b.neg_min, b.min, b.scale, b.qmax
-            e.residual = None if residual is None else residual.data_ptr()
+            if chain is not None:
+                f32, links, relu0 = chain
+                e.residual = None if f32 is None else f32.data_ptr()
+                e.nres, e.res_relu0 = len(links), (1 if relu0 and f32 is None else 0)
+                for l, (code, lbn) in enumerate(links):
+                    lb = self._bn(lbn)
+                    e.res[l] = _lib.ResLink(code=code.data_ptr(), mean=lb.mean, sq=lb.sq, wq=lb.wq, bq=lb.bq,
+                                            min=lb.min, scale=lb.scale)
+            e.bncode_tiled = 1 if bncode_tiled else 0
             e.relu = 1 if relu else 0
             e.out_f32 = None if out_f32 is None else out_f32.data_ptr()
             e.out_bncode = None if out_bncode is None else out_bncode.data_ptr()
@@ -233,7 +252,7 @@ class Engine:
                     setattr(e, f"code{k}_{f}", getattr(co, f))
                 setattr(e, f"out_code{k}", co.ptr)
             assert len(outs) <= 2
-            if bn is not None and residual is None and out_f32 is None and out_bncode is None and len(outs) == 1:
+            if bn is not None and chain is None and out_f32 is None and out_bncode is None and len(outs) == 1:
                 # conv -> RangeBN -> ReLU -> consumer quantizer: one exact per-channel code table
                 lut = torch.empty((cout, 256), dtype=torch.int8, device=self.dev)
                 _lib.call("qnn_bn_code_lut", ctypes.byref(b), cout, 1 if relu else 0, ctypes.byref(outs[0]),
@@ -246,11 +265,6 @@ class Engine:
         self.convs.append((len(self.ops), d, e))
         self._add("qnn_qconv2d_fwd", lambda st: _lib.call("qnn_qconv2d_fwd", xp, wp_, dp, ep, st))
         return Ho, Wo
-
-    def _outputs(self, act, consumers, need_f32):
-        """CodeOut list + fp32 buffer for the producer of `act`."""
-        outs = [self._codes_for(act, c)[1] for c in consumers]
-        return outs, (self._f32_for(act) if need_f32 else None)
 
     # ------------------------------------------------------------------ ResNet
     @staticmethod
@@ -305,6 +319,7 @@ class Engine:
         Ho, Wo = (H + 2 * conv1.padding[0] - kh) // conv1.stride[0] + 1, (W + 2 * conv1.padding[1] - kh) // \
             conv1.stride[1] + 1
         x_act = None
+        ident0 = blocks[0].downsample is None  # block 1 adds the stem's output as its residual
         if has_pool:
             mp = model.maxpool
             pk_, ps_, pp_ = mp.kernel_size, mp.stride, mp.padding
@@ -313,8 +328,12 @@ class Engine:
             self._conv(conv1, src, H, W, bn=bn1, relu=True, out_bncode=bncode)
             Hp_ = (Ho + 2 * pp_ - pk_) // ps_ + 1
             x_act = _Act(Hp_, Hp_, conv1.out_channels)
-            cons, need_f32 = self._block_consumers(blocks[0])
-            outs, f32 = self._outputs(x_act, cons, need_f32)
+            cons, _ = self._block_consumers(blocks[0])
+            outs = [self._codes_for(x_act, c)[1] for c in cons]
+            pcode = None
+            if ident0:  # the pooled RangeBN codes start block 1's residual chain
+                pcode = self._btiled(Hp_, Hp_, conv1.out_channels)
+                x_act.res = (None, [(pcode, bn1)], True)
             b = self._bn(bn1)
             C = conv1.out_channels
             st = _lib.stream_of(self.input)
@@ -327,23 +346,29 @@ class Engine:
             c0 = outs[0] if len(outs) > 0 else None
             c1 = outs[1] if len(outs) > 1 else None
             a = (N, Ho, Wo, C, pk_, ps_, pp_, Hp_, Hp_)
-            fp, qp = _lib.ptr(f32), _lib.ptr(bncode)
+            pc, qp = _lib.ptr(pcode), _lib.ptr(bncode)
             l0 = _lib.ptr(luts[0]) if len(luts) > 0 else None
             l1 = _lib.ptr(luts[1]) if len(luts) > 1 else None
             r0 = None if c0 is None else ctypes.byref(c0)
             r1 = None if c1 is None else ctypes.byref(c1)
             br = ctypes.byref(b)
             self._add("qnn_maxpool_bn", lambda st: _lib.call(
-                "qnn_maxpool_bn", qp, *a, br, 1, fp, 1, l0, r0, l1, r1, st))
+                "qnn_maxpool_bn", qp, *a, br, 1, None, 1, pc, l0, r0, l1, r1, st))
         else:
             x_act = _Act(Ho, Wo, conv1.out_channels)
-            cons, need_f32 = self._block_consumers(blocks[0])
-            outs, f32 = self._outputs(x_act, cons, need_f32)
-            self._conv(conv1, src, H, W, bn=bn1, relu=True, outs=outs, out_f32=f32)
+            cons, _ = self._block_consumers(blocks[0])
+            outs = [self._codes_for(x_act, c)[1] for c in cons]
+            bnc = None
+            if ident0:
+                bnc = self._btiled(Ho, Wo, conv1.out_channels)
+                x_act.res = (None, [(bnc, bn1)], True)
+            self._conv(conv1, src, H, W, bn=bn1, relu=True, outs=outs, out_bncode=bnc, bncode_tiled=True)
         # ---- residual blocks
+        self.block_acts = [x_act]  # the stem output and every block output (inspection)
         for bi, blk in enumerate(blocks):
             nxt = blocks[bi + 1] if bi + 1 < len(blocks) else None
             x_act = self._plan_block(blk, x_act, nxt)
+            self.block_acts.append(x_act)
         # ---- head: avgpool + fc
         self._plan_head(model, x_act, model.avgpool.kernel_size)
 
@@ -354,20 +379,34 @@ class Engine:
         Ho = (x.H - 1) // stride + 1
         Wo = (x.W - 1) // stride + 1
         cout = (blk.conv3 if bottleneck else blk.conv2).out_channels
-        # shortcut
+        # shortcut: a residual code chain (resnet_quantized.py:60-68, :105-113).  The
+        # downsample branch stores only RangeBN's input codes (1 byte) and every consumer
+        # recomputes RangeBN from them; an identity shortcut extends the block input's chain
+        # by this block's own RangeBN codes, so no fp32 map is written or read until a
+        # chain would exceed QNN_MAX_RES links (then this block writes an fp32 checkpoint).
         if blk.downsample is not None:
             ds_conv, ds_bn = blk.downsample[0], blk.downsample[1]
-            r = self._tiled(Ho, Wo, cout)
-            self._conv(ds_conv, self._codes_for(x, ds_conv), x.H, x.W, bn=ds_bn, relu=False, out_f32=r)
-            residual = r
+            code = self._btiled(Ho, Wo, cout)
+            self._conv(ds_conv, self._codes_for(x, ds_conv), x.H, x.W, bn=ds_bn, relu=False, out_bncode=code,
+                       bncode_tiled=True)
+            chain = (None, [(code, ds_bn)], False)
         else:
-            residual = self._f32_for(x)
+            chain = x.res
+            assert chain is not None, "identity shortcut without a residual representation"
         out = _Act(Ho, Wo, cout)
-        if nxt is not None:
-            cons, need_f32 = self._block_consumers(nxt)
-        else:
-            cons, need_f32 = [], True  # the head reads fp32
-        outs, f32 = self._outputs(out, cons, need_f32)
+        last_bn = blk.bn3 if bottleneck else blk.bn2
+        cons = self._block_consumers(nxt)[0] if nxt is not None else []
+        outs = [self._codes_for(out, c)[1] for c in cons]
+        f32 = self._f32_for(out) if nxt is None else None  # the head reads fp32
+        bnc = None
+        if nxt is not None and nxt.downsample is None:  # the next block adds this output
+            f32c, links, relu0 = chain
+            if len(links) < _lib.MAX_RES:
+                bnc = self._btiled(Ho, Wo, cout)
+                out.res = (f32c, links + [(bnc, last_bn)], relu0)
+            else:
+                f32 = self._f32_for(out)
+                out.res = (f32, [], False)
         if bottleneck:
             a1 = _Act(x.H, x.W, blk.conv1.out_channels)
             self._conv(blk.conv1, self._codes_for(x, blk.conv1), x.H, x.W, bn=blk.bn1, relu=True,
@@ -375,14 +414,14 @@ class Engine:
             a2 = _Act(Ho, Wo, blk.conv2.out_channels)
             self._conv(blk.conv2, self._codes_for(a1, blk.conv2), x.H, x.W, bn=blk.bn2, relu=True,
                        outs=[self._codes_for(a2, blk.conv3)[1]])
-            self._conv(blk.conv3, self._codes_for(a2, blk.conv3), Ho, Wo, bn=blk.bn3, residual=residual, relu=True,
-                       outs=outs, out_f32=f32)
+            self._conv(blk.conv3, self._codes_for(a2, blk.conv3), Ho, Wo, bn=blk.bn3, chain=chain, relu=True,
+                       outs=outs, out_f32=f32, out_bncode=bnc, bncode_tiled=True)
         else:
             a1 = _Act(Ho, Wo, blk.conv1.out_channels)
             self._conv(blk.conv1, self._codes_for(x, blk.conv1), x.H, x.W, bn=blk.bn1, relu=True,
                        outs=[self._codes_for(a1, blk.conv2)[1]])
-            self._conv(blk.conv2, self._codes_for(a1, blk.conv2), Ho, Wo, bn=blk.bn2, residual=residual, relu=True,
-                       outs=outs, out_f32=f32)
+            self._conv(blk.conv2, self._codes_for(a1, blk.conv2), Ho, Wo, bn=blk.bn2, chain=chain, relu=True,
+                       outs=outs, out_f32=f32, out_bncode=bnc, bncode_tiled=True)
         return out
 
     def _plan_head(self, model, x, pool_k):
@@ -406,6 +445,40 @@ class Engine:
         self.logits = torch.empty((N, fc.out_features), dtype=torch.float32, device=self.dev)
         geom = dict(hp=1, wp=1, cp=cp, nbytes=nbytes, range=(mn, mx))
         self._conv(fc, (fbuf, co, geom), 1, 1, mode=0, logits=self.logits)
+
+    def untile_codes(self, buf, H, W, C):
+        """Byte C-tile code map (qnn_res_link) -> [N*H*W][C] uint8 (a copy; for tests)."""
+        M = self.N * H * W
+        mt, ct = -(-M // 32), -(-C // 32)
+        t = buf[:mt * ct * 1024].view(mt, ct, 2, 32, 4, 4)  # [mt][ct][fh][m%32][g][u], c = 32ct + 8g + 4fh + u
+        return t.permute(0, 3, 1, 4, 2, 5).reshape(mt * 32, ct * 32)[:M, :C]
+
+    def residual_value(self, act):
+        """The fp32 [N*H*W][C] value act.res encodes, recomputed with torch fp32 ops in the
+        kernels' order (tests: chains must reproduce the module path bitwise)."""
+        f32, links, relu0 = act.res
+        M = self.N * act.H * act.W
+
+        def g(code, bn):
+            b = self._bn(bn)
+            sq, wq, bq = bn._params(bn.running_var)
+            q = self.untile_codes(code, act.H, act.W, act.C).float()
+            t = q * np.float32(b.scale)
+            t = t + np.float32(b.min)
+            t = t - bn.running_mean.float()
+            t = t * sq
+            t = t * wq
+            return t + bq
+
+        if f32 is not None:
+            r, rest = untile(f32, M, act.C), links
+        else:
+            r, rest = g(*links[0]), links[1:]
+            if relu0:
+                r = torch.clamp_min(r, 0.0)
+        for code, bn in rest:
+            r = torch.clamp_min(g(code, bn) + r, 0.0)
+        return r
 
     @property
     def head_input(self):

@@ -50,7 +50,7 @@ def test_bindings_cover_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.qnn_abi_version() == 5
+    assert lib.qnn_abi_version() == 6
 
 
 def test_argument_validation_without_device(lib):
@@ -85,7 +85,8 @@ def test_struct_layout_matches_header():
     from qnn import _lib
     src = open(HEADER).read()
     for cname, py in (("qnn_conv_desc", _lib.ConvDesc), ("qnn_epilogue", _lib.Epilogue),
-                      ("qnn_bn_params", _lib.BnParams), ("qnn_code_out", _lib.CodeOut)):
+                      ("qnn_bn_params", _lib.BnParams), ("qnn_code_out", _lib.CodeOut),
+                      ("qnn_res_link", _lib.ResLink)):
         body = _re.search(r"typedef struct " + cname + r" \{(.*?)\} " + cname, src, _re.S).group(1)
         body = _re.sub(r"/\*.*?\*/", "", body, flags=_re.S)
         names = []
@@ -94,7 +95,7 @@ def test_struct_layout_matches_header():
             if not decl:
                 continue
             decl = _re.sub(r"^(const\s+)?\w+\s*\*?\s*", "", decl)
-            names += [n.strip().lstrip("*") for n in decl.split(",")]
+            names += [_re.sub(r"\[.*\]", "", n.strip().lstrip("*")) for n in decl.split(",")]
         assert names == [f[0] for f in py._fields_], cname
 
 

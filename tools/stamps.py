@@ -33,7 +33,7 @@ def plan(d, e=None):
     e = e if e is not None else _lib.Epilogue(mode=1)
     _lib.call("qnn_conv_plan", ctypes.byref(d), ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(bm),
               ctypes.byref(bn), ctypes.byref(nblk))
-    waves = 8 if cfg.value in (0, 1, 2) else 4
+    waves = [8, 8, 8, 4, 4, 2, 8, 8, 8, 8, 4, 4, 8, 8, 8, 4, 4, 2][cfg.value]  # qconv.hip CFG[].waves
     return cfg.value, waves, nblk.value
 
 
