@@ -35,8 +35,8 @@ __device__ __forceinline__ void decode_pix(int64_t i, int cg, int wo, int ho, in
 }
 
 // ------------------------------------------------------------------ max-pool on RangeBN codes
-// One thread per (output pixel, 16 channels); consecutive lanes take consecutive
-// pixels so the C-tile fp32 stores are 512 contiguous bytes per 32 lanes.  The pool
+// One thread per (output pixel, 16 channels), channel groups fastest (each window tap is
+// one contiguous c-byte read per pixel).  The pool
 // direction per channel (max where g_c increases, min where it decreases) is folded
 // into the codes with an XOR (min q == 255 - max(255 - q)), so the window reduction is
 // a plain bytewise max (two packed-u16 maxes per dword).  RangeBN params and the
@@ -78,31 +78,38 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const uint8_t* __restri
   __syncthreads();
   const int kc = c >> 4, ct = (c + 31) >> 5;
   const int64_t M = (int64_t)n * ho * wo;
-  const int64_t total = ((M + 31) >> 5) * kc * 32;
+  const int64_t total = M * kc;
+  // the 16-channel group is the fastest index: a pixel's c bytes are one contiguous read
   for (int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * blockDim.x) {
-    const int lo = (int)(gi & 31);
-    const int64_t rest = gi >> 5;
-    const int kg = (int)(rest % kc);
-    const int64_t m = (rest / kc) * 32 + lo;
-    if (m >= M) continue;
+    const int kg = (int)(gi % kc);
+    const int64_t m = gi / kc;
     const int cb = 16 * kg;
     const int ox = (int)(m % wo);
     const int64_t t = m / wo;
     const int oy = (int)(t % ho), img = (int)(t / ho);
     const uint4 dm = *reinterpret_cast<const uint4*>(s_dir + cb);
     uint4 best = make_uint4(0, 0, 0, 0);
-    for (int r = 0; r < k; ++r) {
-      const int iy = oy * stride - pad + r;
-      if (iy < 0 || iy >= h) continue;  // MaxPool2d pads with -inf
-      for (int s2 = 0; s2 < k; ++s2) {
-        const int ix = ox * stride - pad + s2;
-        if (ix < 0 || ix >= w) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(q + (((int64_t)img * h + iy) * w + ix) * c + cb);
-        best.x = max_u8x4(best.x, v.x ^ dm.x);
-        best.y = max_u8x4(best.y, v.y ^ dm.y);
-        best.z = max_u8x4(best.z, v.z ^ dm.z);
-        best.w = max_u8x4(best.w, v.w ^ dm.w);
-      }
+    auto tap = [&](int r, int s2) {
+      // MaxPool2d pads with -inf: an out-of-image tap reads a clamped in-image pixel and
+      // is masked to 0, the identity of the folded-code max (all loads issue together)
+      const int iy = oy * stride - pad + r, ix = ox * stride - pad + s2;
+      const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+      const int cy = min(max(iy, 0), h - 1), cx = min(max(ix, 0), w - 1);
+      const uint4 v = *reinterpret_cast<const uint4*>(q + (((int64_t)img * h + cy) * w + cx) * c + cb);
+      const uint32_t msk = ok ? 0xffffffffu : 0u;
+      best.x = max_u8x4(best.x, (v.x ^ dm.x) & msk);
+      best.y = max_u8x4(best.y, (v.y ^ dm.y) & msk);
+      best.z = max_u8x4(best.z, (v.z ^ dm.z) & msk);
+      best.w = max_u8x4(best.w, (v.w ^ dm.w) & msk);
+    };
+    if (k == 3) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2) tap(r, s2);
+    } else {
+      for (int r = 0; r < k; ++r)
+        for (int s2 = 0; s2 < k; ++s2) tap(r, s2);
     }
     const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
     if (out_code) {  // the pooled RangeBN input codes: a residual chain start (byte C-tile)
@@ -341,26 +348,37 @@ __global__ void bn_code_lut_kernel(qnn_bn_params bn, int c, int relu, qnn_code_o
 }
 
 // ------------------------------------------------------------------ avg-pool head
-__global__ void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c, int tiled, float* out_f32,
-                                     qnn_code_out c0) {
-  const int cg = c >> 2;
-  const int64_t total = (int64_t)n * cg;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int g = (int)(i % cg);
-    const int img = (int)(i / cg);
-    const int ct = (c + 31) >> 5;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int t = 0; t < hw; ++t) {
+// Block = (image, 256 channels): lane = 4-channel group, wave w sums pixels w, w+4, ...
+// (several loads in flight per lane), then wave 0 adds the four partial sums in a fixed
+// order and divides by hw (adaptive_avg_pool / AvgPool2d eval; deterministic order).
+__global__ __launch_bounds__(256) void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c,
+                                                            int tiled, float* out_f32, qnn_code_out c0) {
+  __shared__ float4 part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, img = blockIdx.y;
+  const int g = blockIdx.x * 64 + lane, cg = c >> 2, ct = (c + 31) >> 5;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < cg) {
+#pragma unroll 4
+    for (int t = wave; t < hw; t += 4) {
       const int64_t m = (int64_t)img * hw + t;
       const float4 v = *reinterpret_cast<const float4*>(x + (tiled ? ctile_index(m, 4 * g, ct) : m * c + 4 * g));
       s.x = s.x + v.x; s.y = s.y + v.y; s.z = s.z + v.z; s.w = s.w + v.w;
     }
-    const float d = (float)hw;
-    const float val[4] = {s.x / d, s.y / d, s.z / d, s.w / d};
-    if (out_f32)
-      *reinterpret_cast<float4*>(out_f32 + (int64_t)img * c + 4 * g) = make_float4(val[0], val[1], val[2], val[3]);
-    if (c0.ptr) put_code4(c0, img, 0, 0, 4 * g, val);
   }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || g >= cg) return;
+  float4 t = part[0][lane];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const float4 p = part[k][lane];
+    t.x = t.x + p.x; t.y = t.y + p.y; t.z = t.z + p.z; t.w = t.w + p.w;
+  }
+  const float d = (float)hw;
+  const float val[4] = {t.x / d, t.y / d, t.z / d, t.w / d};
+  if (out_f32)
+    *reinterpret_cast<float4*>(out_f32 + (int64_t)img * c + 4 * g) = make_float4(val[0], val[1], val[2], val[3]);
+  if (c0.ptr) put_code4(c0, img, 0, 0, 4 * g, val);
 }
 
 static int grid_for(int64_t work) {
@@ -416,7 +434,7 @@ int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stri
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)maxpool_bn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(maxpool_bn)");
-  const int64_t threads = cdiv((int64_t)n * ho * wo, 32) * (c / 16) * 32;
+  const int64_t threads = (int64_t)n * ho * wo * (c / 16);
   hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(threads)), dim3(256), lds, (hipStream_t)stream, q, n, h, w, c,
                      k, stride, pad, ho, wo, *bn, relu, out_f32, f32_tiled, out_code, has0 ? lut0 : nullptr, c0,
                      has1 ? lut1 : nullptr, c1);
@@ -492,8 +510,9 @@ int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* 
   if (n == 0) return QNN_OK;
   QNN_REQUIRE(x, "null input");
   const qnn_code_out c0 = code0 ? *code0 : none_code();
-  hipLaunchKernelGGL(avgpool_quant_kernel, dim3(grid_for((int64_t)n * (c / 4))), dim3(256), 0, (hipStream_t)stream, x,
-                     n, hw, c, x_tiled, out_f32, c0);
+  QNN_REQUIRE(n < 65536, "batch >= 65536");
+  hipLaunchKernelGGL(avgpool_quant_kernel, dim3((unsigned)cdiv(c / 4, 64), (unsigned)n), dim3(256), 0,
+                     (hipStream_t)stream, x, n, hw, c, x_tiled, out_f32, c0);
   QNN_LAUNCH_CHECK("qnn_avgpool_quant");
   return QNN_OK;
 }
