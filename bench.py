@@ -4,7 +4,7 @@
 Workload (BASELINE.json configs[1]): resnet_quantized depth=18, ImageNet shape
 3x224x224, batch 128 per GPU, int8 MFMA path, synthetic inputs resident in HBM.
 A "step" is one forward of one batch (plus, at N>1, the RCCL gather of the
-logits to rank 0).  Weak scaling: every rank processes its own 128 images.
+logits to rank 0, issued asynchronously and drained inside the timed region).  Weak scaling: every rank processes its own 128 images.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -112,6 +112,43 @@ def cpu_baseline(model_cpu_sd, depth, batch, iters, threads, arch="resnet"):
                       f"torch {torch.__version__} CPU, {threads} threads, {platform.processor() or platform.machine()}"}
 
 
+def timed_run(step, steps, warmup, world, sync=None):
+    """The contract's timed region: `warmup` untimed steps, then barrier + sync, exactly
+    `steps` steps, every step's in-flight gather drained (`.result()`), barrier + sync;
+    returns the MAX over ranks of the elapsed seconds.  `step()` returns a
+    ShardedInference handle (or None); `sync` is the device synchronize (None on CPU)."""
+    sync = sync or (lambda: None)
+
+    def fence():
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+
+    with torch.no_grad():
+        for h in [step() for _ in range(warmup)]:
+            if h is not None:
+                h.result()
+        fence()
+        t0 = time.perf_counter()
+        for h in [step() for _ in range(steps)]:
+            if h is not None:
+                h.result()
+        fence()
+        elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def throughput(global_batch, steps, elapsed):
+    """Whole-job images/s: every rank's images of every timed step over the slowest rank's time."""
+    return global_batch * steps / elapsed
+
+
 def model_name(arch, depth):
     return "mobilenet" if arch == "mobilenet" else f"resnet{depth}"
 
@@ -163,28 +200,10 @@ def main():
     engine.input.copy_(synthetic.input_batch((args.batch, 3, 224, 224), 1234 + rank).to(device))
     runner = qdist.ShardedInference(engine, args.batch * world)
 
-    def step():
-        return runner(engine.input)
+    def step():  # one graph replay + the asynchronous logits gather (overlaps the next replay)
+        return runner.submit(engine.input)
 
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = timed_run(step, args.steps, args.warmup, world, torch.cuda.synchronize)
 
     # Per-launch HIP-event timing of every kernel of one forward (eager pass over the
     # same launch sequence the graph replays; events on the launch stream)
@@ -217,14 +236,13 @@ def main():
             module_ips = args.batch * max(2, args.steps // 4) / (time.perf_counter() - t1)
 
     if rank == 0:
-        images = args.batch * world * args.steps
         ms_per_step = elapsed / args.steps * 1e3
         achieved = mfma_ops / (conv_ms_per_fwd * 1e-3) / 1e12
         pmc = pmc_traffic(args.model, args.depth, args.batch)
         nconv = sum(1 for n in engine.launch_names if n == "qnn_qconv2d_fwd")
         line = {
             "metric": METRIC,
-            "value": round(images / elapsed, 2),
+            "value": round(throughput(args.batch * world, args.steps, elapsed), 2),
             "unit": "images/s",
             "n_gpus": world,
             "steps": args.steps,

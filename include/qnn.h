@@ -235,6 +235,30 @@ int qnn_dwconv2d_fwd(const float* x, int n, int c, int h, int w, const float* w_
                      int sh, int sw, int ph, int pw, int ho, int wo, float neg_min, float min, float scale,
                      float qmax, const float* bias, float* y, qnn_stream_t stream);
 
+/* ---------------------------------------------------------------- calibration (§8(f2)) */
+
+/* QuantMeasure's train-branch statistics (models/modules/quantize.py:225-236) of x viewed
+ * as [rows][row_len] (rows = batch, input_.view(input_.size(0), -1)):
+ *   out[0] = mean over rows of min(row)      (:226-227)
+ *   out[1] = mean over rows of max(row)      (:229-230)
+ *   out[2] = mean(x), out[3] = std(x, unbiased)   (:232-233)
+ * Deterministic fixed-order reductions accumulated in fp64 (the reference reduces in fp32
+ * torch order; agreement ~1e-6 relative).  The caller applies the momentum updates
+ * (:216-219) and the aciq range (:238-239).  work: qnn_measure_stats_work(rows) doubles of
+ * device scratch.  Replaces the torch reductions of QuantMeasure.forward in training mode. */
+int64_t qnn_measure_stats_work(int64_t rows);
+int qnn_measure_stats_f32(const float* x, int64_t rows, int64_t row_len, double* work, float* out,
+                          qnn_stream_t stream);
+
+/* RangeBN's train-branch statistics (quantize.py:466-472) of x [b][c][hw] (NCHW): per
+ * channel c, over the sequence q = bi*hw + p (x.transpose(0, 1) flattened) split into
+ * num_chunks equal chunks:
+ *   mean_max[c] = mean_k max(chunk k)   mean_min[c] = mean_k min(chunk k)   mean[c] = mean(q)
+ * b*hw % num_chunks == 0 (the reference's view).  The caller forms scale (:473-476) and the
+ * momentum updates (:478-482).  work: 3 * c * num_chunks doubles. */
+int qnn_rangebn_stats_f32(const float* x, int b, int c, int hw, int num_chunks, double* work, float* mean_max,
+                          float* mean_min, float* mean, qnn_stream_t stream);
+
 /* ---------------------------------------------------------------- RangeBN */
 
 /* RangeBN.forward eval for NCHW fp32 (quantize.py:461-505):

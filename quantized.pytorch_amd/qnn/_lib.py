@@ -87,6 +87,8 @@ SIGNATURES = {
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],
+    "qnn_measure_stats_f32": [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr],
+    "qnn_rangebn_stats_f32": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr, c_int, c_ptr],
 }
@@ -125,6 +127,8 @@ def load(path=None):
     v = lib.qnn_abi_version()
     if v != ABI_VERSION:
         raise QnnLibraryError(f"qnn: ABI version mismatch (library {v}, bindings {ABI_VERSION})")
+    lib.qnn_measure_stats_work.restype = c_i64
+    lib.qnn_measure_stats_work.argtypes = [c_i64]
     lib.qnn_conv_tile_count.restype = c_int
     lib.qnn_conv_tile_count.argtypes = []
     if lib.qnn_conv_tile_count() != CONV_TILES:

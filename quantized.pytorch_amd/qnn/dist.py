@@ -9,7 +9,14 @@ the outputs to device 0.  Here:
   * each rank owns a contiguous slice of the global batch (inputs generated or
     loaded on that rank's device);
   * the only data-path collective is ONE gather of the logits to rank 0 over
-    RCCL (`torch.distributed` backend "nccl" is RCCL on ROCm; xGMI on MI355X).
+    RCCL (`torch.distributed` backend "nccl" is RCCL on ROCm; xGMI on MI355X),
+    issued asynchronously (`submit`): the logits are copied into one of two send
+    slots and the gather overlaps the next step's forward;
+  * calibration (main.py:154-205, measure mode) runs on every rank's own batches
+    and `allreduce_calibration` merges the running ranges with ONE bucketed
+    all-reduce (the reference's DataParallel keeps replica 0's statistics only,
+    main.py:345; averaging equal-count running averages is the statistic of all
+    ranks' batches).
 The shard/gather logic is backend-agnostic and is tested with `gloo` on CPU.
 """
 import os
@@ -48,12 +55,58 @@ def shard_bounds(global_batch, world, rank):
     return start, start + base + (1 if rank < rem else 0)
 
 
+def allreduce_calibration(model, group=None):
+    """Average every calibrated statistic of `model` over the ranks of `group`: the
+    running_min / running_max / running_mean / running_var of each QuantMeasure and the
+    running_mean / running_var of each RangeBN, flattened into one fp32 bucket and
+    all-reduced once (RCCL on GPU tensors, gloo on CPU).  Call after every rank ran the
+    same number of measure-mode batches.  No-op for world size 1."""
+    from .quantize import QuantMeasure, RangeBN
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    bufs = []
+    for m in model.modules():
+        if isinstance(m, QuantMeasure):
+            bufs += [m.running_min, m.running_max, m.running_mean, m.running_var]
+        elif isinstance(m, RangeBN):
+            bufs += [m.running_mean, m.running_var]
+    if not bufs:
+        return
+    flat = torch.cat([b.detach().reshape(-1).to(torch.float32) for b in bufs])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat /= dist.get_world_size(group)
+    off = 0
+    with torch.no_grad():
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off:off + n].view_as(b))
+            off += n
+
+
+class _Pending:
+    """An in-flight gather (ShardedInference.submit): result() waits and returns the
+    [global_batch, ...] logits on root, None elsewhere."""
+
+    def __init__(self, work, fn):
+        self._work, self._fn, self._out, self._done = work, fn, None, False
+
+    def result(self):
+        if not self._done:
+            if self._work is not None:
+                self._work.wait()
+            self._out, self._done = self._fn(), True
+        return self._out
+
+
 class ShardedInference:
     """Run `model` on this rank's shard and gather the logits on `root`.
 
     `__call__(x_local)` returns the full [global_batch, ...] output on root and
-    None elsewhere.  Ragged shards are padded to the largest shard for the
-    collective and trimmed on root.
+    None elsewhere.  `submit(x_local)` issues the same gather asynchronously and
+    returns a handle (`.result()`): the logits are first copied into one of two send
+    slots, so the caller may start the next forward (which overwrites an engine's
+    static logits) while the collective runs.  Ragged shards are padded to the
+    largest shard for the collective and trimmed on root.
     """
 
     def __init__(self, model, global_batch, root=0, group=None):
@@ -65,7 +118,8 @@ class ShardedInference:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.bounds = [shard_bounds(global_batch, self.world, r) for r in range(self.world)]
         self.max_shard = max(e - s for s, e in self.bounds)
-        self._gather_bufs = None
+        self._slots = {}  # shape -> [(send, recv list, pending handle)] x 2
+        self._k = 0
         planned = getattr(model, "N", None)  # a qnn.Engine runs exactly the batch it was built for
         if planned is not None:
             s, e = self.bounds[self.rank]
@@ -76,25 +130,41 @@ class ShardedInference:
     def local_slice(self):
         return self.bounds[self.rank]
 
-    def gather(self, y_local):
+    def submit_output(self, y_local):
+        """Start gathering this rank's output `y_local`; returns a _Pending."""
         if self.world == 1:
-            return y_local
+            return _Pending(None, lambda: y_local)
         n_local = y_local.shape[0]
         s, e = self.bounds[self.rank]
         assert n_local == e - s, f"rank {self.rank}: expected a shard of {e - s}, got {n_local}"
-        if n_local != self.max_shard:
-            pad = y_local.new_zeros((self.max_shard - n_local,) + tuple(y_local.shape[1:]))
-            y_send = torch.cat([y_local, pad])
-        else:
-            y_send = y_local.contiguous()
+        shape = (self.max_shard,) + tuple(y_local.shape[1:])
+        slots = self._slots.get(shape)
+        if slots is None:
+            slots = self._slots[shape] = [None, None]
+        k = self._k % 2
+        self._k += 1
+        if slots[k] is None:
+            send = y_local.new_zeros(shape)
+            recv = [torch.empty_like(send) for _ in range(self.world)] if self.rank == self.root else None
+            slots[k] = [send, recv, None]
+        send, recv, prev = slots[k]
+        if prev is not None:
+            prev.result()  # the gather that used this slot two submits ago has finished
+        send[:n_local].copy_(y_local)  # ordered before the collective on the current stream
+        work = dist.gather(send, recv, dst=self.root, group=self.group, async_op=True)
         if self.rank == self.root:
-            if self._gather_bufs is None or self._gather_bufs[0].shape != y_send.shape:
-                self._gather_bufs = [torch.empty_like(y_send) for _ in range(self.world)]
-            dist.gather(y_send, self._gather_bufs, dst=self.root, group=self.group)
-            parts = [b[: e - s] for b, (s, e) in zip(self._gather_bufs, self.bounds)]
-            return torch.cat(parts)
-        dist.gather(y_send, None, dst=self.root, group=self.group)
-        return None
+            fn = lambda: torch.cat([b[: e_ - s_] for b, (s_, e_) in zip(recv, self.bounds)])
+        else:
+            fn = lambda: None
+        slots[k][2] = pend = _Pending(work, fn)
+        return pend
+
+    def gather(self, y_local):
+        return self.submit_output(y_local).result()
+
+    def submit(self, x_local):
+        with torch.no_grad():
+            return self.submit_output(self.model(x_local))
 
     def __call__(self, x_local):
         with torch.no_grad():

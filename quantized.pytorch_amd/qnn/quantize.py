@@ -140,6 +140,35 @@ class QuantNode:
                     q.overwrite_params(logging)
 
 
+def measure_stats(x):
+    """QuantMeasure's batch statistics (quantize.py:226-233) on the device: 0-dim fp32
+    tensors (mean of per-sample min, mean of per-sample max, mean, unbiased std)."""
+    _require_device(x, "QuantMeasure calibration")
+    xc = x.detach().contiguous()
+    B = xc.size(0)
+    lib = _lib.load()
+    work = torch.empty(lib.qnn_measure_stats_work(B), dtype=torch.float64, device=xc.device)
+    out = torch.empty(4, dtype=torch.float32, device=xc.device)
+    _lib.call("qnn_measure_stats_f32", _lib.ptr(xc), B, xc.numel() // B, _lib.ptr(work), _lib.ptr(out),
+              _lib.stream_of(xc))
+    return out[0], out[1], out[2], out[3]
+
+
+def rangebn_stats(x, num_chunks):
+    """RangeBN's train reductions (quantize.py:467-472) on the device: per-channel
+    (mean of chunk maxima, mean of chunk minima, mean) and the chunk length."""
+    _require_device(x, "RangeBN calibration")
+    xc = x.detach().contiguous()
+    B, C, H, W = xc.shape
+    if (B * H * W) % num_chunks:
+        raise ValueError(f"qnn: RangeBN statistics need B*H*W % num_chunks == 0 (got {B * H * W}, {num_chunks})")
+    work = torch.empty(3 * C * num_chunks, dtype=torch.float64, device=xc.device)
+    mm, mn, mean = (torch.empty(C, dtype=torch.float32, device=xc.device) for _ in range(3))
+    _lib.call("qnn_rangebn_stats_f32", _lib.ptr(xc), B, C, H * W, num_chunks, _lib.ptr(work), _lib.ptr(mm),
+              _lib.ptr(mn), _lib.ptr(mean), _lib.stream_of(xc))
+    return mm, mn, mean, B * H * W // num_chunks
+
+
 class QuantMeasure(nn.Module, QuantNode):
     """quantize.py:198-268: per-tensor activation range; eval = running range."""
     _QMEASURE_SUPPORTED_METHODS = ["avg", "aciq"]
@@ -164,13 +193,12 @@ class QuantMeasure(nn.Module, QuantNode):
         running_stat.mul_(momentum).add_(new_value * (1 - momentum))
 
     def _observe(self, input_):
-        """Train-branch statistics (quantize.py:225-239); returns the batch range."""
-        min_value = input_.view(input_.size(0), -1).min(-1)[0].mean()
+        """Train-branch statistics (quantize.py:225-239); returns the batch range.  The
+        reductions run in one device pass (qnn_measure_stats_f32); the momentum updates
+        are the reference's torch ops."""
+        min_value, max_value, mean, std = measure_stats(input_)
         self._momentum_update_stat(min_value, self.running_min)
-        max_value = input_.view(input_.size(0), -1).max(-1)[0].mean()
         self._momentum_update_stat(max_value, self.running_max)
-        mean = input_.mean()
-        std = input_.std(unbiased=True)
         self._momentum_update_stat(mean, self.running_mean)
         self._momentum_update_stat(std, self.running_var)
         self.num_measurements += 1
@@ -678,13 +706,9 @@ class RangeBN(nn.Module):
         if x.dim() == 2:
             x = x.unsqueeze(-1).unsqueeze(-1)
         if self.training:
-            B, C, H, W = x.shape
-            y = x.transpose(0, 1).contiguous()
-            y = y.view(C, self.num_chunks, B * H * W // self.num_chunks)
-            mean_max = y.max(-1)[0].mean(-1)
-            mean_min = y.min(-1)[0].mean(-1)
-            mean = y.view(C, -1).mean(-1)
-            scale_fix = (0.5 * 0.35) * (1 + (math.pi * math.log(4)) ** 0.5) / ((2 * math.log(y.size(-1))) ** 0.5)
+            # the chunked reductions in one device pass (qnn_rangebn_stats_f32), the rest op for op
+            mean_max, mean_min, mean, n = rangebn_stats(x, self.num_chunks)
+            scale_fix = (0.5 * 0.35) * (1 + (math.pi * math.log(4)) ** 0.5) / ((2 * math.log(n)) ** 0.5)
             scale = 1 / ((mean_max - mean_min) * scale_fix + self.eps)
             self.running_mean.detach().mul_(self.momentum).add_(mean * (1 - self.momentum))
             self.running_var.detach().mul_(self.momentum).add_(scale * (1 - self.momentum))

@@ -2,7 +2,9 @@
 
 The GPU path is the same code with backend "nccl" (RCCL); only the collective's
 transport differs.  Checks: contiguous ragged sharding, gather-to-root equals
-the unsharded forward, non-root ranks get None, batch independence.
+the unsharded forward, non-root ranks get None, batch independence; the asynchronous
+double-buffered gather over a static-buffer engine through bench.py's timed region;
+the bucketed all-reduce of calibrated ranges.
 """
 import os
 import socket
@@ -65,3 +67,120 @@ def test_gather_matches_unsharded_world2(gb):
         assert p.exitcode == 0
     res = dict(q.get(timeout=10) for _ in range(2))
     assert res == {"root": True, "other": True}
+
+
+class _StaticEngine:
+    """Stands in for qnn.Engine on CPU: planned for exactly N samples, returns its static
+    logits buffer (the next call overwrites it), as Engine.__call__ does."""
+
+    def __init__(self, n, w):
+        self.N, self.w = n, w
+        self.logits = torch.empty(n, w.shape[1])
+
+    def __call__(self, x):
+        assert x.shape[0] == self.N
+        torch.matmul(x, self.w, out=self.logits)
+        return self.logits
+
+
+def _engine_worker(rank, world, port, gb, steps, q):
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = torch.randn(16, 5, generator=torch.Generator().manual_seed(3))
+    xs = [torch.randn(gb, 16, generator=torch.Generator().manual_seed(100 + k)) for k in range(steps)]
+    s, e = shard_bounds(gb, world, rank)
+    eng = _StaticEngine(e - s, w)
+    runner = ShardedInference(eng, gb)
+    # every step in flight before any result is read: the double-buffered send slots keep
+    # each step's logits although the engine's static buffer is overwritten by the next step
+    handles = [runner.submit(x[s:e]) for x in xs]
+    outs = [h.result() for h in handles]
+    ok = all(o is None for o in outs) if rank else \
+        all(torch.allclose(o, x @ w, rtol=0, atol=1e-5) for o, x in zip(outs, xs))
+    # bench.py's timed region + aggregation over the same runner
+    k = iter(range(10 ** 6))
+    elapsed = bench.timed_run(lambda: runner.submit(xs[next(k) % steps][s:e]), steps, 1, world)
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    same = t.item() == elapsed  # MAX over ranks: every rank reports the same time
+    q.put((rank, ok, same, bench.throughput(gb, steps, elapsed) == gb * steps / elapsed))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("gb", [7, 129])
+def test_sharded_engine_async_gather_ragged_world2(gb):
+    """ShardedInference over a static-buffer engine per rank (ragged shards 4/3 and 65/64),
+    driven through bench.py's timed_run / throughput."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, 2, port, gb, 4, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert res == [(0, True, True, True), (1, True, True, True)]
+
+
+def _calib_worker(rank, world, port, q):
+    from oracle import qnn_oracle as O
+    from qnn import synthetic
+    from qnn.dist import allreduce_calibration
+    from qnn.quantize import QConv2d, RangeBN
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = torch.nn.Sequential(QConv2d(4, 8, 3, padding=1, bias=False), RangeBN(8))
+
+    def states(r):  # each rank calibrates on its own two batches (the oracle's statistics)
+        qm, rb = O.measure_state(), {"running_mean": torch.zeros(8), "running_var": torch.zeros(8),
+                                     "measure": O.measure_state()}
+        for j in range(2):
+            O.calibrate_measure(qm, synthetic.input_batch((3, 4, 6, 6), 500 + 10 * r + j))
+            O.calibrate_rangebn(rb, synthetic.input_batch((4, 8, 6, 6), 700 + 10 * r + j))
+        return qm, rb
+
+    qm, rb = states(rank)
+    with torch.no_grad():
+        for k, v in qm.items():
+            getattr(model[0].quantize_input, k).copy_(v)
+        model[1].running_mean.copy_(rb["running_mean"])
+        model[1].running_var.copy_(rb["running_var"])
+        for k, v in rb["measure"].items():
+            getattr(model[1].quantize_input, k).copy_(v)
+    allreduce_calibration(model)
+    both = [states(r) for r in range(world)]
+    ok = True
+    for k in ("running_min", "running_max", "running_mean", "running_var"):
+        want = sum(s[0][k] for s in both) / world
+        ok &= torch.allclose(getattr(model[0].quantize_input, k), want, rtol=1e-6, atol=0)
+    for k in ("running_mean", "running_var"):
+        ok &= torch.allclose(getattr(model[1], k), sum(s[1][k] for s in both) / world, rtol=1e-6, atol=0)
+    # running-average momentum: the merged range is the one-process calibration over all batches
+    seq = O.measure_state()
+    for r in range(world):
+        for j in range(2):
+            O.calibrate_measure(seq, synthetic.input_batch((3, 4, 6, 6), 500 + 10 * r + j))
+    ok &= torch.allclose(model[0].quantize_input.running_min, seq["running_min"], rtol=1e-6, atol=0)
+    ok &= torch.allclose(model[0].quantize_input.running_max, seq["running_max"], rtol=1e-6, atol=0)
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_calibration_world2():
+    """qnn.dist.allreduce_calibration averages every QuantMeasure / RangeBN running
+    statistic over the ranks in one all-reduce."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calib_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert sorted(q.get(timeout=10) for _ in range(2)) == [(0, True), (1, True)]
