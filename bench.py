@@ -88,28 +88,63 @@ def build(device, depth, seed=11, arch="resnet"):
     return model
 
 
-def cpu_baseline(model_cpu_sd, depth, batch, iters, threads, arch="resnet"):
-    """Oracle (the reference's fake-quant CPU forward, restated) on a bounded sample."""
+def cpu_model_name():
+    """The host CPU model (lscpu's "Model name", from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_threads():
+    """(threads used, affinity cores): every core of this process's affinity mask, capped
+    at the box's CPU share (OMP_NUM_THREADS, set to the per-GPU share on the GPU box,
+    where the affinity mask spans the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", aff) or aff)
+    return max(1, min(aff, share)), aff
+
+
+def cpu_baseline(model_cpu_sd, depth, batch, iters, threads, arch="resnet", warmup=2, config_batch=None):
+    """Oracle (the reference's fake-quant CPU forward, restated and pinned bitwise to it)
+    on a bounded sample: `warmup` untimed forwards, then the median of
+    `iters`, with the reference's biprecision double contraction and, separately, one
+    contraction per layer."""
     from oracle import qnn_oracle as O
     from qnn import synthetic
     torch.set_num_threads(threads)
     x = synthetic.input_batch((batch, 3, 224, 224), 4242)
     sd = {k: v.clone() for k, v in model_cpu_sd.items()}
     kw = dict(depth=depth, dataset="imagenet") if arch == "resnet" else {}
-    O.model_forward(sd, x, arch, kw)  # warm-up
-    times = []
-    t_end = time.perf_counter() + 30.0
-    for _ in range(iters):
-        t0 = time.perf_counter()
-        O.model_forward(sd, x, arch, kw)
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() > t_end:
-            break
-    med = float(np.median(times))
+
+    def median_s(biprecision):
+        with O.contraction(biprecision=biprecision):
+            for _ in range(warmup):
+                O.model_forward(sd, x, arch, kw)
+            times = []
+            for _ in range(iters):
+                t0 = time.perf_counter()
+                O.model_forward(sd, x, arch, kw)
+                times.append(time.perf_counter() - t0)
+        return float(np.median(times))
+
+    med, med1 = median_s(True), median_s(False)
+    cb = config_batch or batch
     return {"value": round(batch / med, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/qnn_oracle.py {model_name(arch, depth)} imagenet fake-quant forward (biprecision double conv, "
-                      f"as the reference), batch {batch}, median of {len(times)} after 1 warm-up, "
-                      f"torch {torch.__version__} CPU, {threads} threads, {platform.processor() or platform.machine()}"}
+            "sample": f"oracle/qnn_oracle.py {model_name(arch, depth)} imagenet fake-quant forward (biprecision "
+                      f"double conv, as the reference), batch {batch}, median of {iters} after {warmup} warm-ups, "
+                      f"torch {torch.__version__} CPU, {threads} threads",
+            "cpu_model": cpu_model_name(), "affinity_cores": len(os.sched_getaffinity(0)),
+            "batch": batch, "s_per_batch": round(med, 4),
+            "extrapolation": None if cb == batch else
+            f"images/s measured at batch {batch}, reported for the batch-{cb} config: the CPU forward is a "
+            f"sequence of batched ops whose time is linear in the batch (per-image rate)",
+            "single_conv": {"value": round(batch / med1, 3), "unit": "images/s", "s_per_batch": round(med1, 4),
+                            "note": "one contraction per layer instead of the reference's out1 + out2 - out1"}}
 
 
 def timed_run(step, steps, warmup, world, sync=None):
@@ -177,8 +212,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--depth", type=int, default=18)
     ap.add_argument("--model", choices=("resnet", "mobilenet"), default="resnet")
-    ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-iters", type=int, default=5)
+    ap.add_argument("--cpu-batch", type=int, default=32, help="CPU baseline batch (BASELINE.md §4: b32)")
+    ap.add_argument("--cpu-iters", type=int, default=5, help="CPU baseline timed forwards (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--module-path", type=int, default=1, help="also time the per-module drop-in path (N=1)")
     args = ap.parse_args()
@@ -271,10 +306,10 @@ def main():
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:
-            threads = min(16, len(os.sched_getaffinity(0)))
+            threads, _ = cpu_threads()
             sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
             line["cpu_baseline"] = cpu_baseline(sd, args.depth, args.cpu_batch, args.cpu_iters, threads,
-                                                arch=args.model)
+                                                arch=args.model, config_batch=args.batch)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -18,7 +18,15 @@ Fixtures hold data only (numpy .npz, loadable with allow_pickle=False):
   * model_<name>.npz   - whole-model logits (cifar/imagenet ResNet-18, ResNet-50,
                          MobileNet) + every calibrated buffer
 
-Usage: python tools/gen_golden.py [--only NAME ...]
+The files are byte-for-byte reproducible (`savez`: fixed zip metadata; every input from
+seeds): tools/check_golden.sh regenerates into a scratch directory and compares hashes.
+
+Note on weight_min/weight_max (and bias_min/bias_max): in measure mode the reference skips
+the block that refreshes them (enable_quant is False, quantize.py:316-330), so after
+calibration they still hold the min/max of torch's default initialisation under
+torch.manual_seed(0) -- which is what the fixtures record; eval forwards recompute them.
+
+Usage: python tools/gen_golden.py [--only NAME ...] [--out DIR]
 """
 import argparse
 import json
@@ -38,6 +46,21 @@ import refload  # noqa: E402
 from qnn import synthetic  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden")
+
+
+def savez(path, **arrays):
+    """np.savez_compressed with reproducible bytes: fixed zip timestamps and modes, entries
+    in insertion order (numpy's own writer stamps the current time).  np.load reads it."""
+    import io
+    import zipfile
+    with zipfile.ZipFile(path, "w", compression=zipfile.ZIP_DEFLATED) as zf:
+        for k, v in arrays.items():
+            buf = io.BytesIO()
+            np.lib.format.write_array(buf, np.asanyarray(v), allow_pickle=False)
+            zi = zipfile.ZipInfo(k + ".npy", date_time=(1980, 1, 1, 0, 0, 0))
+            zi.compress_type = zipfile.ZIP_DEFLATED
+            zi.external_attr = 0o644 << 16
+            zf.writestr(zi, buf.getvalue())
 
 # --------------------------------------------------------------------------- layers
 # (name, kind, ctor kwargs, input shape, calib relu?, eval relu?)
@@ -117,7 +140,7 @@ def gen_quantize_kat(Q):
         b = synthetic.uniform((n,), -0.1, 0.3, 3000, i)
         rec[f"none/{i}/x"] = b
         rec[f"none/{i}/y"] = Q.quantize(torch.from_numpy(b), num_bits=8).numpy()
-    np.savez_compressed(os.path.join(OUT, "quantize_kat.npz"), **rec)
+    savez(os.path.join(OUT, "quantize_kat.npz"), **rec)
     print("quantize_kat:", len(rec), "arrays")
 
 
@@ -145,7 +168,7 @@ def gen_layer(Q, name, kind, kw, shape, relu_in):
            "y": y.numpy(), "param_checksum": np.array(synthetic.param_checksum(wrap)),
            "x_checksum": np.array(float(x.double().abs().sum()))}
     rec.update(bufs)
-    np.savez_compressed(os.path.join(OUT, f"layer_{name}.npz"), **rec)
+    savez(os.path.join(OUT, f"layer_{name}.npz"), **rec)
     print(f"layer_{name}: y{tuple(y.shape)} max|y|={y.abs().max():.4g}")
 
 
@@ -166,14 +189,17 @@ def gen_model(Q, RQ, MQ, name, fac, kw, shape, calib_b):
            "logits": logits.numpy(), "param_checksum": np.array(synthetic.param_checksum(model)),
            "keys": np.array(list(model.state_dict().keys()))}
     rec.update(bufs)
-    np.savez_compressed(os.path.join(OUT, f"model_{name}.npz"), **rec)
+    savez(os.path.join(OUT, f"model_{name}.npz"), **rec)
     print(f"model_{name}: logits{tuple(logits.shape)} argmax={logits.argmax(1).tolist()}")
 
 
 def main():
+    global OUT
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*")
+    ap.add_argument("--out", default=OUT, help="output directory (default tests/golden)")
     a = ap.parse_args()
+    OUT = a.out
     torch.set_num_threads(max(1, min(8, os.cpu_count() or 1)))
     Q, RQ, MQ = refload.load()
     os.makedirs(OUT, exist_ok=True)
