@@ -296,7 +296,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": f"qconv_kernel (all {nconv} QConv2d/QLinear launches of one forward)",
                          "achieved": round(achieved, 2), "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_INT8_TOPS, 4),
-                         "traffic": None if pmc is None else pmc["hbm_bytes_per_forward"],
+                         "traffic": None if pmc is None else pmc.get("conv_hbm_bytes_per_forward",
+                                                                      pmc["hbm_bytes_per_forward"]),
                          "traffic_source": None if pmc is None else pmc["source"],
                          "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
                          "model_frac": round(total_ops / (ms_per_step * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4)},

@@ -88,6 +88,7 @@ class Engine:
         self.ops = []
         self.keep = []
         self.launch_names = []
+        self.launch_meta = []
         self.convs = []  # (op index, ConvDesc, Epilogue) of every contraction
         self._bn_cache = {}  # RangeBN module -> BnParams: each module's range is read exactly once
         with torch.no_grad():
@@ -189,9 +190,12 @@ class Engine:
             return False
 
     # ------------------------------------------------------------------ ops
-    def _add(self, name, fn):
+    def _add(self, name, fn, ops=0, nbytes=0, shape=None):
+        """Append a launch.  ops / nbytes: its algorithmic int8 ops and minimum HBM bytes
+        (every operand read once, every output written once) for roofline accounting."""
         self.ops.append(fn)
         self.launch_names.append(name)
+        self.launch_meta.append({"kernel": name, "ops": int(ops), "bytes": int(nbytes), "shape": shape})
 
     def _conv(self, conv, src, H, W, bn=None, chain=None, relu=False, outs=(), out_f32=None, out_bncode=None,
               bncode_tiled=False, mode=1, logits=None):
@@ -263,7 +267,15 @@ class Engine:
         self.keep += [pk, sxsw, sxbw, table, g, d, e, xbuf]
         xp, wp_, dp, ep = _lib.ptr(xbuf), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e)
         self.convs.append((len(self.ops), d, e))
-        self._add("qnn_qconv2d_fwd", lambda st: _lib.call("qnn_qconv2d_fwd", xp, wp_, dp, ep, st))
+        M = self.N * Ho * Wo
+        ops = 2 * M * cout * cin // (conv.groups if isinstance(conv, QConv2d) else 1) * kh * kw
+        out_b = M * cout * ((4 if out_f32 is not None or mode == 0 else 0) + len(outs) +
+                            (1 if out_bncode is not None else 0))
+        if chain is not None:
+            out_b += M * cout * ((4 if chain[0] is not None else 0) + len(chain[1]))
+        nbytes = geom["nbytes"] + pk.cout_pad * pk.kpad + out_b
+        self._add("qnn_qconv2d_fwd", lambda st: _lib.call("qnn_qconv2d_fwd", xp, wp_, dp, ep, st), ops, nbytes,
+                  [M, cout, kh * kw * cin])
         return Ho, Wo
 
     # ------------------------------------------------------------------ ResNet
@@ -305,7 +317,8 @@ class Engine:
             args = (N, 3, H, W, ph, hz, hz, -float(mn), s, q)
             zp = _lib.ptr(zbuf)
             self._add("qnn_quantize_nchw_to_s2d8",
-                      lambda st: _lib.call("qnn_quantize_nchw_to_s2d8", xin, zp, *args, st))
+                      lambda st: _lib.call("qnn_quantize_nchw_to_s2d8", xin, zp, *args, st), 0,
+                      N * 3 * H * W * 4 + nbytes, [N, 3, H, W])
         else:
             stem_act = _Act(H, W, 3)
             src = self._codes_for(stem_act, conv1)
@@ -314,7 +327,8 @@ class Engine:
             args = (N, 3, H, W, geom["pad"], geom["cp"], co.neg_min, s, q)
             bp = _lib.ptr(buf)
             self._add("qnn_quantize_nchw_to_nhwc8",
-                      lambda st: _lib.call("qnn_quantize_nchw_to_nhwc8", xin, bp, *args, st))
+                      lambda st: _lib.call("qnn_quantize_nchw_to_nhwc8", xin, bp, *args, st), 0,
+                      N * 3 * H * W * 4 + geom["nbytes"], [N, 3, H, W])
         # ---- stem conv (+ bn1 + relu [+ maxpool])
         Ho, Wo = (H + 2 * conv1.padding[0] - kh) // conv1.stride[0] + 1, (W + 2 * conv1.padding[1] - kh) // \
             conv1.stride[1] + 1
@@ -353,7 +367,9 @@ class Engine:
             r1 = None if c1 is None else ctypes.byref(c1)
             br = ctypes.byref(b)
             self._add("qnn_maxpool_bn", lambda st: _lib.call(
-                "qnn_maxpool_bn", qp, *a, br, 1, None, 1, pc, l0, r0, l1, r1, st))
+                "qnn_maxpool_bn", qp, *a, br, 1, None, 1, pc, l0, r0, l1, r1, st), 0,
+                N * Ho * Wo * C + N * Hp_ * Hp_ * C * (len(outs) + (1 if pcode is not None else 0)),
+                [N, Ho, Wo, C])
         else:
             x_act = _Act(Ho, Wo, conv1.out_channels)
             cons, _ = self._block_consumers(blocks[0])
@@ -441,7 +457,8 @@ class Engine:
         self._head = (src, x.H, x.W, x.C)
         hw = k * k
         sp, cr, C = _lib.ptr(src), ctypes.byref(co), x.C
-        self._add("qnn_avgpool_quant", lambda st: _lib.call("qnn_avgpool_quant", sp, N, hw, C, 1, None, cr, st))
+        self._add("qnn_avgpool_quant", lambda st: _lib.call("qnn_avgpool_quant", sp, N, hw, C, 1, None, cr, st), 0,
+                  N * hw * C * 4 + N * cp, [N, hw, C])
         self.logits = torch.empty((N, fc.out_features), dtype=torch.float32, device=self.dev)
         geom = dict(hp=1, wp=1, cp=cp, nbytes=nbytes, range=(mn, mx))
         self._conv(fc, (fbuf, co, geom), 1, 1, mode=0, logits=self.logits)
@@ -506,7 +523,8 @@ class Engine:
         xin, s, q = _lib.ptr(self.input), float_scale(mn, mx, stem.num_bits), _qmax(stem.num_bits)
         args = (N, 3, H, W, ph, hz, hz, -float(mn), s, q)
         zp = _lib.ptr(zbuf)
-        self._add("qnn_quantize_nchw_to_s2d8", lambda st: _lib.call("qnn_quantize_nchw_to_s2d8", xin, zp, *args, st))
+        self._add("qnn_quantize_nchw_to_s2d8", lambda st: _lib.call("qnn_quantize_nchw_to_s2d8", xin, zp, *args, st),
+                  0, N * 3 * H * W * 4 + nbytes, [N, 3, H, W])
         x = _Act(Ho, Ho, stem.out_channels)
         self._conv(stem, ("s2d", zbuf, dict(hp=hz, wp=hz, cp=16, nbytes=nbytes, range=(mn, mx))), H, W, bn=stem_bn,
                    relu=True, outs=[self._codes_for(x, blocks[0][0])[1]])
@@ -529,7 +547,9 @@ class Engine:
             dargs2 = (k, k, st, st, Ho, Ho, float(dmn), x_scale)
             qb, xbp, wtp, br, pr = _lib.ptr(pk.qbias), _lib.ptr(xb), _lib.ptr(wt), ctypes.byref(b), ctypes.byref(pco)
             self._add("qnn_dwconv_fused", lambda st, xbp=xbp, wtp=wtp, dargs=dargs, dargs2=dargs2, qb=qb, br=br, pr=pr:
-                      _lib.call("qnn_dwconv_fused", xbp, *dargs, wtp, *dargs2, qb, br, 1, None, pr, st))
+                      _lib.call("qnn_dwconv_fused", xbp, *dargs, wtp, *dargs2, qb, br, 1, None, pr, st),
+                      2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4,
+                      [N, Ho, Ho, x.C])
             # pointwise + bn + relu -> next dw codes (or fp32 for the head)
             out = _Act(Ho, Ho, pw.out_channels)
             if last:

@@ -4,6 +4,7 @@ consumer's quantizer, include/qnn.h qnn_dwconv_fused).
 The 3x3 fast kernel (dwconv3_kernel: 8 channels x 4 pixels per thread, register
 weights, division-free quantizers) restates the generic kernel's arithmetic op for
 op, so both must agree BITWISE on every output (fp32 and codes) — over strides 1/2,
+larger maps and
 ragged widths (wo not a multiple of 4), channel counts whose c/8 does not divide 256,
 with and without bias / RangeBN.  The fp32 output is also held to the per-layer bar
 against an fp64 restatement of the reference's depthwise conv (quantize.py:343,
@@ -40,6 +41,10 @@ def _run(xcodes, geom, wt, bias, bn, relu, out_f32, code, generic, st):
     (1, 9, 24, 1, False, False),   # c/8 = 3 does not divide 256; wo = 9
     (2, 11, 40, 2, True, False),   # ragged, stride 2
     (4, 28, 256, 2, False, True),
+    (2, 56, 128, 1, True, True),
+    (1, 112, 32, 1, True, True),
+    (2, 29, 64, 2, True, True),    # odd extent, stride 2
+    (1, 15, 96, 1, False, True),
 ])
 def test_dwconv_fast_equals_generic_bitwise(gpu, n, h, c, s, with_bias, with_bn):
     g = torch.Generator().manual_seed(1000 + c + h)
