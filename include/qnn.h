@@ -222,10 +222,12 @@ int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc
 int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn, int* nblk);
 
 /* Number of tile configurations (valid qnn_conv_desc.tile values are 1 .. count).  Those with
- * ids >= 12 are the halo-band kernels for kh x kw > 1: the block's input rows are read into
+ * ids 12-25 are the halo-band kernels for kh x kw > 1: the block's input rows are read into
  * LDS once per K chunk and every tap reads them at a shifted LDS address (no im2col
- * re-reads from L2).  An explicit tile that is not built for the layer / epilogue kind is an
- * argument error. */
+ * re-reads from L2); ids 26-29 the resident-band kernels (whole output rows per block, the
+ * band of ALL input channels loaded once, weights streamed straight into registers, no
+ * barrier in the K loop; kh x kw > 1, cp % 64 == 0).  An explicit tile that is not built for
+ * the layer / epilogue kind is an argument error. */
 int qnn_conv_tile_count(void);
 
 /* Depthwise (groups == cin == cout) eval forward: fake-quantize-on-load of x

@@ -28,11 +28,12 @@ def main():
     ap.add_argument("--model", choices=("resnet", "mobilenet"), default="resnet")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--tile", type=int, default=None, help="force this tile configuration where it is built")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     _lib.load()
     model = bench.build(dev, a.depth, arch=a.model)
-    eng = Engine(model, batch=a.batch, graph=False)
+    eng = Engine(model, batch=a.batch, graph=False, tile=a.tile)
     eng.input.copy_(synthetic.input_batch((a.batch, 3, 224, 224), 1234).to(dev))
     descs = [k for k in eng.keep if isinstance(k, _lib.ConvDesc)]
     epis = [k for k in eng.keep if isinstance(k, _lib.Epilogue)]

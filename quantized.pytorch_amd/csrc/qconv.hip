@@ -1451,9 +1451,11 @@ static const CfgInfo CFG[NCFG] = {
 };
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
-static int ncfg_all() { return NCFG + q16_count(); }
+static int ncfg_all() { return NCFG + q16_count() + rb_count(); }
+static int rb_first() { return NCFG + q16_count(); }
 
 static bool cfg_ok(int k, const Params& p) {
+  if (k >= rb_first()) return rb_ok(k - rb_first(), p);
   if (k >= NCFG) return q16_ok(k - NCFG, p);
   if (k < 0) return false;
   const int ek = epi_kind(p.e);
@@ -1468,6 +1470,7 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
+  if (k >= rb_first()) return rb_cost(k - rb_first(), p);
   if (k >= NCFG) return q16_cost(k - NCFG, p);
   const CfgInfo& c = CFG[k];
   const int64_t tiles = cdiv(p.M, c.bn) * cdiv(p.d.cout, c.bm);
@@ -1497,6 +1500,7 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (k >= rb_first()) return rb_launch(k - rb_first(), x, w, p, s);
   if (k >= NCFG) return q16_launch(k - NCFG, x, w, p, s);
   switch (k) {
     case 0: return launch_ek<C0>(x, w, p, s);
@@ -1578,11 +1582,12 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   int tbm, tbn;
-  if (k >= NCFG) q16_tile(k - NCFG, &tbm, &tbn);
+  if (k >= rb_first()) rb_tile(k - rb_first(), &tbm, &tbn);
+  else if (k >= NCFG) q16_tile(k - NCFG, &tbm, &tbn);
   else tbm = CFG[k].bm, tbn = CFG[k].bn;
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
-  if (nblk) *nblk = (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm));
+  if (nblk) *nblk = k >= rb_first() ? (int)rb_blocks(k - rb_first(), p) : (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm));
   return QNN_OK;
 }
 

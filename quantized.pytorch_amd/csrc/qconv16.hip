@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "qconv_common.h"
+#include "epi16.h"
 
 #ifndef QNN_ABLATE
 #define QNN_ABLATE 0  // diagnostic builds only (make ablate): 1 no weight loads, 2 no MFMA, 3 no epilogue
@@ -92,126 +93,6 @@ __device__ __forceinline__ void wait_rt(int n) {
     }
 }
 
-// y of 4 consecutive channels cl..cl+3 (local) of one pixel: the exact decomposition with the
-// op order of qconv.hip's conv_out4p (fma(sw, acc, fma(bw, psq, tb)) + bias), packed pairs.
-__device__ __forceinline__ void conv_out4(const float* s_f, int BM, int cl, int ptab, float psq, const v4i& a,
-                                          f2 (&v)[2]) {
-  const float4 sw = *reinterpret_cast<const float4*>(s_f + cl);
-  const float4 bw = *reinterpret_cast<const float4*>(s_f + BM + cl);
-  const float4 tb = *reinterpret_cast<const float4*>(s_f + ptab + cl);
-  const float4 bi = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
-  const f2 p2 = {psq, psq};
-  const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
-  v[0] = pfma((f2){sw.x, sw.y}, a01, pfma((f2){bw.x, bw.y}, p2, (f2){tb.x, tb.y})) + (f2){bi.x, bi.y};
-  v[1] = pfma((f2){sw.z, sw.w}, a23, pfma((f2){bw.z, bw.w}, p2, (f2){tb.z, tb.w})) + (f2){bi.z, bi.w};
-}
-
-struct Pix {  // one output pixel of a lane
-  int m, n, ho, wo;
-  bool ok;
-};
-
-// Epilogue over the 16x16 accumulator layout: acc[i][j] lane l holds channels
-// c0 + wm*16*TM + 16i + 4(l>>4) + r (r = 0..3) of pixel m0 + wn*16*TN + 16j + (l&15).
-template <class C, int EK>
-__device__ __forceinline__ void epilogue16(const Params& p, const v4i (&acc)[C::TM][C::TN], const int (&sumq)[C::TN],
-                                           const int (&pcls)[C::TN], const Pix (&pix)[C::TN], const int8_t* smem,
-                                           int c0, int wm, int lane) {
-  constexpr int BM = C::BM, TM = C::TM, TN = C::TN;
-  const qnn_conv_desc& d = p.d;
-  const qnn_epilogue& e = p.e;
-  const int g = lane >> 4;
-  const int HoWo = d.ho * d.wo;
-  const float* s_f = reinterpret_cast<const float*>(smem + p.epi_off);
-  const int nparam = 7 * BM;
-  const int8_t* s_lut = smem + p.epi_off + 4 * (7 + e.nclass) * BM;
-  const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
-  const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
-  const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
-  const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
-  const bool has_res = EK == EK_GEN && e.residual != nullptr;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const Pix& P = pix[j];
-    const int ptab = nparam + pcls[j] * BM;
-    const float psq = (float)sumq[j];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int cl = wm * 16 * TM + 16 * i + 4 * g;  // local channel of register 0
-      const int c = c0 + cl;
-      const bool cok = c < d.cout;                   // fused modes: cout % 16 == 0 (4-channel groups all in)
-      f2 v[2];
-      conv_out4(s_f, BM, cl, ptab, psq, acc[i][j], v);
-      if constexpr (EK == EK_NCHW) {  // drop-in QConv2d output, NCHW fp32
-        if (P.ok) {
-          float* yp = e.out_f32 + ((int64_t)P.n * d.cout + c) * HoWo + P.ho * d.wo + P.wo;
-          const float y4[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (c + r < d.cout) yp[(int64_t)r * HoWo] = y4[r];
-        }
-      } else if constexpr (EK == EK_LUT) {  // conv -> RangeBN -> ReLU -> consumer quantizer, tabulated
-        const f2 q0 = qclamp2(v[0], bnp) + MAGIC_U8, q1 = qclamp2(v[1], bnp) + MAGIC_U8;
-        const unsigned qq[4] = {__float_as_uint(q0.x) & 255u, __float_as_uint(q0.y) & 255u,
-                                __float_as_uint(q1.x) & 255u, __float_as_uint(q1.y) & 255u};
-        int rr = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rr |= ((int)(uint8_t)s_lut[(cl + u) * 256 + qq[u]]) << (8 * u);
-        if (P.ok && c < e.code0_cp)
-          *reinterpret_cast<int*>(e.out_code0 + (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp +
-                                                 P.wo + e.code0_pad) * e.code0_cp + c) = cok ? rr : 0;
-      } else if constexpr (EK == EK_BNCODE) {
-        const int rr = pack4(qclamp2(v[0], bnp) + MAGIC_U8, qclamp2(v[1], bnp) + MAGIC_U8);
-        if (P.ok && cok) *reinterpret_cast<int*>(e.out_bncode + (int64_t)P.m * d.cout + c) = rr;
-      } else {  // EK_GEN: [RangeBN] [+ residual] [ReLU] -> fp32 and/or codes x2
-        if (e.bn_mean) {
-          const f2 qb[2] = {qclamp2(v[0], bnp), qclamp2(v[1], bnp)};
-          const float4 mn4 = *reinterpret_cast<const float4*>(s_f + 3 * BM + cl);
-          const float4 sq4 = *reinterpret_cast<const float4*>(s_f + 4 * BM + cl);
-          const float4 wq4 = *reinterpret_cast<const float4*>(s_f + 5 * BM + cl);
-          const float4 bq4 = *reinterpret_cast<const float4*>(s_f + 6 * BM + cl);
-          const f2 mn[2] = {{mn4.x, mn4.y}, {mn4.z, mn4.w}}, sq[2] = {{sq4.x, sq4.y}, {sq4.z, sq4.w}};
-          const f2 wq[2] = {{wq4.x, wq4.y}, {wq4.z, wq4.w}}, bq[2] = {{bq4.x, bq4.y}, {bq4.z, bq4.w}};
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            f2 o = rint2(qb[h]) * bn_s2;  // dequant: q * s
-            o = o + bn_m2;                // + min
-            o = o - mn[h];                // x - mean
-            o = o * sq[h];                // * q(scale)
-            o = o * wq[h];                // * q(weight)
-            v[h] = o + bq[h];             // + q(bias)
-          }
-        }
-        const int mc = P.ok ? P.m : p.M - 1;
-        const int cc = cok ? c : d.cout - 4;
-        if (has_res) {
-          const int64_t fi = e.f32_tiled ? ctile_index(mc, cc, p.ct) : (int64_t)mc * d.cout + cc;
-          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + fi);
-          v[0] = v[0] + (f2){r4.x, r4.y};
-          v[1] = v[1] + (f2){r4.z, r4.w};
-        }
-        if (e.relu) {
-          v[0].x = fmaxf(v[0].x, 0.f); v[0].y = fmaxf(v[0].y, 0.f);
-          v[1].x = fmaxf(v[1].x, 0.f); v[1].y = fmaxf(v[1].y, 0.f);
-        }
-        if (e.out_f32 && P.ok && cok) {
-          const int64_t fi = e.f32_tiled ? ctile_index(P.m, c, p.ct) : (int64_t)P.m * d.cout + c;
-          *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
-        }
-        if (e.out_code0 && P.ok && c < e.code0_cp) {
-          const int k0 = cok ? pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8) : 0;
-          *reinterpret_cast<int*>(e.out_code0 + (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp +
-                                                 P.wo + e.code0_pad) * e.code0_cp + c) = k0;
-        }
-        if (e.out_code1 && P.ok && c < e.code1_cp) {
-          const int k1 = cok ? pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8) : 0;
-          *reinterpret_cast<int*>(e.out_code1 + (((int64_t)P.n * e.code1_hp + P.ho + e.code1_pad) * e.code1_wp +
-                                                 P.wo + e.code1_pad) * e.code1_cp + c) = k1;
-        }
-      }
-    }
-  }
-}
 
 template <class C, int EK, int NPL, bool MASKED>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv16_kernel(

@@ -136,5 +136,12 @@ void q16_tile(int k, int* bm, int* bn);
 bool q16_ok(int k, const Params& p);
 double q16_cost(int k, const Params& p);
 int q16_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s);
+// qconv_rb.hip's resident-band configurations (ids after qconv16.hip's)
+int rb_count();
+void rb_tile(int k, int* bm, int* bn);
+bool rb_ok(int k, const Params& p);
+double rb_cost(int k, const Params& p);
+int64_t rb_blocks(int k, const Params& p);
+int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s);
 
 }  // namespace qnn

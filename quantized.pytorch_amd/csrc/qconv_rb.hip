@@ -1,0 +1,668 @@
+// Resident-band int8 convolution on v_mfma_i32_16x16x64_i8: the eval forward of QConv2d
+// (models/modules/quantize.py:314-349) for kh x kw > 1, same exact decomposition and
+// epilogue arithmetic as qconv.hip / qconv16.hip, so every configuration
+// of every kernel family computes bitwise identical outputs.
+//
+// A block owns whole output rows -- one or more images, or a divisor of an image's rows --
+// and BM output channels.  Its input BAND (every padded input row those output rows read,
+// ALL Cp channels) is loaded into LDS once, at kernel start, by LDS-DMA; every tap of every
+// K step then reads its B fragment at a tap-shifted LDS address.  No input byte crosses L2
+// more than once per block (qconv.hip's implicit im2col pulls it once per tap), and the
+// main loop has no barrier at all:
+//
+// * B = the band, 32-byte PLANES (plane v = bytes [32v, 32v + 32) of every band pixel,
+//   planes 1 KiB aligned).  A 16x16x64 fragment lane (pixel l&15, K bytes 16*(l>>4)..) reads
+//   plane 2g + (l>>5), half (l>>4)&1, of its pixel: within each ds_read_b128 lane group the
+//   16 (pixel, half) pairs land on 16 distinct bank slots (2*pixel + half mod 16) -- no
+//   swizzle, no padding; a tap shift is one uniform add.  Tiles that straddle an output row
+//   end see at most 2-way conflicts.
+// * A = the weights straight from the packed rows ([cout_pad][kpad], tap-major) into VGPRs,
+//   one global_load_dwordx4 per 16-channel tile per K step, prefetched DA steps ahead.  Each
+//   wave owns its own output channels, so nothing is shared and nothing synchronises.  K
+//   steps run plane-pair major (g = 2gp, 2gp+1 for each tap), so the two loads of a pair
+//   consume each 128-byte weight line whole, back to back.
+// * sum_valid(q'_x): per band pixel channel sums after the loop, then the taps' sum per
+//   output pixel (padding codes are 0, so the receptive-field sum is exact).
+#include <stdlib.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "qconv_common.h"
+#include "epi16.h"
+
+#ifndef QNN_ABLATE
+#define QNN_ABLATE 0  // diagnostic builds only: 1 no weight loads, 2 no MFMA, 3 no epilogue
+#endif
+#ifndef QNN_RB_ASM
+#define QNN_RB_ASM 1  // 1: band reads as inline asm with hand-counted lgkmcnt; 0: compiler-scheduled
+#endif
+#ifndef QNN_STAMP
+#define QNN_STAMP 0  // diagnostic builds only (make stamp_rb): per-wave s_memtime phase stamps
+#endif
+#if QNN_STAMP
+// [block][wave][8]: realtime start/end, cycles: band landed, K loop, sums, late staging, epilogue
+// code, store drain
+__device__ unsigned long long qnn_rb_stamps[1 << 18];
+#define RB_TS(v)                                                                          \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+#else
+#define RB_TS(v) ((void)0)
+#endif
+
+namespace qnn {
+namespace rb {
+
+template <class F, int... J>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// s_waitcnt lgkmcnt(N) for the hand-counted inline-asm LDS reads; the scheduling barrier keeps
+// the compiler from hoisting register-only MFMAs above it
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// WGM x WGN waves; a wave owns TM 16-channel tiles x TN 16-pixel tiles; DA K steps of
+// weights in flight per wave; BPC blocks per CU the registers and LDS must allow.
+template <int WGM_, int WGN_, int TM_, int TN_, int DA_, int BPC_>
+struct Cfg {
+  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, DA = DA_, BPC = BPC_;
+  static constexpr int W = WGM * WGN, NT = 64 * W;
+  static constexpr int BM = WGM * TM * 16;  // output channels per block
+  static constexpr int BN = WGN * TN * 16;  // pixel columns per block (>= the block's pixels)
+};
+
+constexpr int NBW_MAX = 16;  // band DMA pieces per wave
+
+struct Geo {
+  int rows;       // flattened output rows (n*ho) per block
+  int npx;        // output pixels per block (rows * wo)
+  int nbands;     // blocks along the pixels
+  int nbrows;     // padded input rows of a band
+  int wb, we, s2; // band row width (>= wp, padded so (sh*wb - wo) % 8 == 0 when LDS allows: a 16-pixel
+                  // tile straddling an output row then keeps its 16 distinct bank slots);
+                  // stride 2: even columns first, we = (wp + 1) / 2
+  int nbp;        // band pixels (nbrows * wb)
+  int pl;         // bytes per 32-byte plane (1 KiB multiple)
+  int npl;        // planes (cp / 32)
+  int ppp;        // 1 KiB DMA pieces per plane
+  int nbw;        // band DMA pieces per wave
+  int pg0, nbw0;  // planes of group 0 (the first plane pair's, or all) and its DMA per wave
+  int nrest;      // later pieces per wave, issued in the first rp0 K steps (kernel SP per step,
+  int rp, rp0;    //   the u-th at rest index step + u*rp0); rp = SP (0: no split)
+  int dummy_off;  // LDS: the KiB the dummy DMA land in
+  int lut;        // EK_LUT: the 256-byte-per-channel code table is staged (else evaluated)
+  int psum_off;   // LDS: int channel sum of each band pixel
+  int tap_off;    // LDS: int band offset (pixels) of each tap
+  int cls_off;    // LDS: int hcls[ho] * nwc, then wcls[wo]
+  int main_bytes; // LDS of the main loop (band + psum + taps)
+};
+
+// ---------------------------------------------------------------- kernel
+// SP: band pieces issued per K step (0: the whole band before the loop; 1 or 2: the first
+// plane pair's planes before it, the rest SP per step, every step issuing exactly SP DMA --
+// dummies past the rest -- so every weight wait stays a compile-time vmcnt)
+template <class C, int EK, int H, int SP>
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_rb_kernel(
+    const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
+  constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+
+  const qnn_conv_desc& d = p.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+#if QNN_STAMP
+  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0, ts6 = 0;
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+  RB_TS(ts0);
+#endif
+
+  // ---- XCD-aware bijective block -> (band, channel tile) map, channel tiles fastest
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nblk = g.nbands * nby;
+  int t;
+  {
+    const int bb = blockIdx.x, xcd = bb & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bb >> 3);
+  }
+  const int band = t / nby;
+  const int c0 = (t - band * nby) * BM;
+  const int r0 = band * g.rows;              // first flattened output row
+  const int nrows_all = d.n * d.ho;
+  const int R0 = (r0 / d.ho) * d.hp + (r0 % d.ho) * d.sh;  // first padded input row (batch-flat)
+  const int rows_in = d.n * d.hp;
+
+  // ---- band DMA: a piece is 1 KiB of plane v = band pixels [32r, 32r + 32) (range r), lane i
+  // pixel + (i >> 1), 16-byte half i & 1.  A wave issues every plane of a range back to back
+  // (ranges r = wave + W*j), so the 4 pieces reading one 128-byte pixel line hit L1 after the
+  // first.  Ranges past the band re-read the last one (identical bytes to the same place).
+  auto band_src = [&](int r, int v) -> uint32_t {
+    int b = r * 32 + (lane >> 1);
+    b = b < g.nbp ? b : g.nbp - 1;
+    const int br = b / g.wb, cc = b - br * g.wb;
+    const int col = g.s2 ? (cc < g.we ? 2 * cc : 2 * (cc - g.we) + 1) : cc;
+    int row = R0 + br;
+    row = row < rows_in ? row : rows_in - 1;  // past the batch: feeds only pixels never stored
+    if (cc >= d.wp) return (uint32_t)d.zero_off;  // row padding of the band (never read)
+    return (uint32_t)((row * d.wp + col) * d.cp + 32 * v + 16 * (lane & 1));
+  };
+  auto band_dst = [&](int r, int v) -> int8_t* { return smem + v * g.pl + r * 1024; };
+  auto issue_piece = [&](int r, int v) {
+    r = r < g.ppp ? r : g.ppp - 1;
+    uint32_t off = band_src(r, v);
+    asm volatile("" : "+v"(off));
+    __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)band_dst(r, v), 16, 0, 0);
+  };
+  // group 0 (planes [0, pg0): the first plane pair's, or all) now
+  for (int k = 0; k < g.nbw0; ++k) issue_piece(wave + W * (k / g.pg0), k % g.pg0);
+  // the epilogue's data next (EK_LUT: with its code table when g.lut, else evaluated)
+  auto stage = [&] {
+    if (EK == EK_LUT && g.lut) stage_epi<C, EK_LUT>(p, x, smem + p.epi_off, c0, wave, lane);
+    else stage_epi<C, (EK == EK_LUT ? EK_BNCODE : EK)>(p, x, smem + p.epi_off, c0, wave, lane);
+  };
+  if (p.epi_early) stage();
+  auto issue_rest = [&](int s) {  // branch-free: exactly SP DMA
+    const int pr = g.npl - g.pg0;     // planes of the rest
+#pragma unroll
+    for (int u = 0; u < SP; ++u) {
+      const int k = s + u * g.rp0;  // this wave's u-th rest piece of step s
+      const bool real = s < g.rp0 && k < g.nrest;
+      int r = wave + W * (k / pr);
+      r = r < g.ppp ? r : g.ppp - 1;
+      const int v = g.pg0 + k % pr;
+      uint32_t off = band_src(r, v);
+      off = real ? off : (uint32_t)d.zero_off;  // dummies: the zero page into the dummy KiB
+      asm volatile("" : "+v"(off));
+      int8_t* dst = real ? band_dst(r, v) : smem + g.dummy_off;
+      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)dst, 16, 0, 0);
+    }
+  };
+
+  // ---- this lane's pixels: block pixel q = (wn*TN + j)*16 + (lane & 15); past the block
+  // (or the batch) they stand in for the block's last pixel and are never stored
+  const int npx_blk = __builtin_amdgcn_readfirstlane(
+      (r0 + g.rows <= nrows_all ? g.rows : nrows_all - r0) * d.wo);
+  int pb[TN];  // band pixel of tap (0, 0), in bytes of a plane (x32)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int q = (wn * TN + j) * 16 + (lane & 15);
+    q = q < npx_blk ? q : npx_blk - 1;
+    const int rr = q / d.wo, col = q - rr * d.wo;
+    const int r = r0 + rr, n = r / d.ho, ho = r - n * d.ho;
+    pb[j] = ((n * d.hp + ho * d.sh - R0) * g.wb + col) * 32 + (lane >> 5) * g.pl + 16 * ((lane >> 4) & 1);
+  }
+
+  // ---- weights: rows c0 + wm*16*TM + 16*i + (lane & 15), K bytes 16*(lane >> 4) of each step
+  const int8_t* wblk = w + (int64_t)c0 * d.kpad;
+  uint32_t aoff[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int row = wm * 16 * TM + 16 * i + (lane & 15);
+    row = c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0;
+    aoff[i] = (uint32_t)(row * d.kpad + 16 * (lane >> 4));
+  }
+
+  // K steps: plane pairs gp (H = 2 64-byte channel groups each; H = 1 when cp == 64), taps t,
+  // h in the pair: step (g = H*gp + h, t) is weight bytes t*cp + 64g and band planes 2g, 2g+1
+  const int KS = (d.cp / 64) * p.taps;
+  struct Cur {
+    int t, tr, tc, gp, h;
+  };
+  auto advance = [&](Cur& c) {
+    if (++c.h == H) {
+      c.h = 0;
+      if (++c.tc == d.kw) c.tc = 0, ++c.tr;
+      if (++c.t == p.taps) c.t = 0, c.tr = 0, c.tc = 0, ++c.gp;
+    }
+  };
+  auto kbytes = [&](const Cur& c) { return c.t * d.cp + 64 * (H * c.gp + c.h); };
+
+  v4i fa[DA][TM];
+  Cur cl = {0, 0, 0, 0, 0};  // the next step to load
+  auto load_a = [&](v4i (&dst)[TM]) {
+    if (QNN_ABLATE == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) dst[i] = (v4i){i, 1, 2, 3};
+      return;
+    }
+    const int kb = kbytes(cl);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const v4i*>(wblk + kb + aoff[i]);
+    if (H * cl.gp + cl.h < d.cp / 64 - 1 || cl.t < p.taps - 1 || cl.h < H - 1) advance(cl);  // clamp at the last step
+  };
+#pragma unroll
+  for (int s = 0; s < DA; ++s) load_a(fa[s]);
+  // LDS constants and the epilogue's data (their loads wait behind the band and the weights)
+  int* s_tap = reinterpret_cast<int*>(smem + g.tap_off);
+  int* s_hc = reinterpret_cast<int*>(smem + g.cls_off);  // border classes: hcls[ho] * nwc, wcls[wo]
+  if (tid < p.taps) {
+    const int tr = tid / d.kw, tc = tid - tr * d.kw;
+    s_tap[tid] = tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc);
+  }
+  for (int i = tid; i < d.ho + d.wo; i += NT)
+    s_hc[i] = i < d.ho ? p.e.hcls[i] * p.e.nwc : p.e.wcls[i - d.ho];
+
+  v4i acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+
+  // the band's group 0, the weights and the epilogue data have landed for this wave
+  wait_vmcnt<0>();
+  __syncthreads();
+#if QNN_STAMP
+  RB_TS(ts1);
+#endif
+
+  Cur cc = {0, 0, 0, 0, 0};
+  int ks = 0;  // K steps done
+  // One K step: the TN band fragments are read up front (inline asm, so the compiler
+  // cannot interleave each read with its first use), then each fragment's TM MFMAs wait
+  // only for that fragment (LDS returns in order: lgkmcnt(TN-1-j)).  The partner wave on
+  // the SIMD runs its MFMAs while this one waits for its reads.
+  auto step = [&](auto slotc, auto dmac) {
+    constexpr int SL = decltype(slotc)::value;
+    constexpr bool DMA = decltype(dmac)::value;
+    const int dt = cc.tr * g.wb + (g.s2 ? (cc.tc & 1) * g.we + (cc.tc >> 1) : cc.tc);
+    const int boff = (2 * (H * cc.gp + cc.h)) * g.pl + 32 * dt;
+    v4i fb[TN];
+#if QNN_RB_ASM
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      v4i r;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(pb[j] + boff));
+      fb[j] = r;
+    }
+#else
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const v4i*>(smem + pb[j] + boff);
+    __builtin_amdgcn_sched_group_barrier(0x100, TN, 0);       // the TN band reads first
+    __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);  // then the MFMAs
+#endif
+    static_for<TN>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+#if QNN_RB_ASM
+      lds_wait<TN - 1 - j>();
+#endif
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (QNN_ABLATE == 2) {
+          asm volatile("" ::"v"(fa[SL][i]), "v"(fb[j]));
+          acc[i][j][0] += fa[SL][i].x;
+        } else {
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[SL][i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    });
+    if constexpr (DMA) issue_rest(ks);  // older than the weights loaded next: landed DA steps later
+    load_a(fa[SL]);
+    advance(cc);
+    ++ks;
+  };
+  auto run = [&](int nsteps, auto dmac) {
+#pragma nounroll
+    for (int k0 = 0; k0 < nsteps; k0 += DA) {
+      step(std::integral_constant<int, 0>{}, dmac);
+      if constexpr (DA > 1) step(std::integral_constant<int, 1>{}, dmac);
+      if constexpr (DA > 2) step(std::integral_constant<int, 2>{}, dmac);
+      if constexpr (DA > 3) step(std::integral_constant<int, 3>{}, dmac);
+    }
+  };
+  if constexpr (SP > 0) {
+    // plane pair 0 with the rest of the band streaming in, then every wave's rest has landed
+    run(H * p.taps, std::true_type{});
+    wait_vmcnt<DA*(TM + SP)>();
+    __syncthreads();
+    run(KS - H * p.taps, std::false_type{});
+  } else {
+    run(KS, std::false_type{});
+  }
+
+#if QNN_STAMP
+  RB_TS(ts2);
+#endif
+  // ---- sum_valid(q'_x): channel sums of every band pixel, then each output pixel's taps
+  int* s_ps = reinterpret_cast<int*>(smem + g.psum_off);
+  for (int b = tid; b < g.nbp; b += NT) {
+    int sm[4] = {0, 0, 0, 0};  // independent chains (exact integer sums in any order)
+#pragma unroll 2
+    for (int v = 0; v < g.npl; ++v) {
+      const v4i a = *reinterpret_cast<const v4i*>(smem + v * g.pl + 32 * b);
+      const v4i c = *reinterpret_cast<const v4i*>(smem + v * g.pl + 32 * b + 16);
+      sm[0] = __builtin_amdgcn_sdot4(a.x, 0x01010101, sm[0], false);
+      sm[1] = __builtin_amdgcn_sdot4(a.y, 0x01010101, sm[1], false);
+      sm[2] = __builtin_amdgcn_sdot4(a.z, 0x01010101, sm[2], false);
+      sm[3] = __builtin_amdgcn_sdot4(a.w, 0x01010101, sm[3], false);
+      sm[0] = __builtin_amdgcn_sdot4(c.x, 0x01010101, sm[0], false);
+      sm[1] = __builtin_amdgcn_sdot4(c.y, 0x01010101, sm[1], false);
+      sm[2] = __builtin_amdgcn_sdot4(c.z, 0x01010101, sm[2], false);
+      sm[3] = __builtin_amdgcn_sdot4(c.w, 0x01010101, sm[3], false);
+    }
+    s_ps[b] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+  }
+  __syncthreads();
+  int sumq[TN], b0[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    sumq[j] = 0;
+    b0[j] = (pb[j] - (lane >> 5) * g.pl) >> 5;  // band pixel of tap (0, 0)
+  }
+  {
+    int tr = 0, tc = 0;
+    for (int tt = 0; tt < p.taps; ++tt) {  // per tap: TN independent reads
+      const int dt = tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sumq[j] += s_ps[b0[j] + dt];
+      if (++tc == d.kw) tc = 0, ++tr;
+    }
+  }
+  wait_vmcnt<0>();  // the clamped tail weight loads
+  __syncthreads();  // the band and sums are dead: the epilogue may stage over them
+#if QNN_STAMP
+  RB_TS(ts3);
+#endif
+  if (QNN_ABLATE == 3) {
+    int z = sumq[0];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z ^= acc[i][j][r];
+    if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;
+    return;
+  }
+  if (!p.epi_early) {
+    stage();
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+#if QNN_STAMP
+  RB_TS(ts5);
+#endif
+  {
+    const int HoWo = d.ho * d.wo;
+    // this lane's pixel of tile j, stepped from tile j-1 (the epilogue visits j in order):
+    // one division for tile 0, then +16 with carries; pixels past the block take its last
+    int cq = (wn * TN) * 16 + (lane & 15);
+    int cm = r0 * d.wo + (cq < npx_blk ? cq : npx_blk - 1);
+    int cn = cm / HoWo, cho = (cm - cn * HoWo) / d.wo, cwo = cm - cn * HoWo - cho * d.wo;
+    const int lm = r0 * d.wo + npx_blk - 1;
+    const int ln = lm / HoWo, lho = (lm - ln * HoWo) / d.wo, lwo = lm - ln * HoWo - lho * d.wo;
+    auto pixel = [&](int j, q16::Pix& P, int& pc) {
+      if (j > 0) {
+        cq += 16;
+        cwo += 16;
+        while (cwo >= d.wo) {
+          cwo -= d.wo;
+          if (++cho == d.ho) cho = 0, ++cn;
+        }
+      }
+      P.ok = cq < npx_blk;
+      P.m = P.ok ? r0 * d.wo + cq : lm;
+      P.n = P.ok ? cn : ln;
+      P.ho = P.ok ? cho : lho;
+      P.wo = P.ok ? cwo : lwo;
+      pc = s_hc[P.ho] + s_hc[d.ho + P.wo];
+    };
+    q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
+  }
+#if QNN_STAMP
+  RB_TS(ts6);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  RB_TS(ts4);
+  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && blockIdx.x < (1 << 18) / (8 * W)) {
+    unsigned long long* o = qnn_rb_stamps + ((size_t)blockIdx.x * W + wave) * 8;
+    o[0] = rt0; o[1] = rt1; o[2] = ts1 - ts0; o[3] = ts2 - ts1; o[4] = ts3 - ts2; o[5] = ts5 - ts3;
+    o[6] = ts6 - ts5; o[7] = ts4 - ts6;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------- host side
+// Rows per block: whole images when an image fits the pixel columns, else the largest
+// divisor of ho that does (so no block straddles an image and every band has the same
+// height) and whose band fits LDS.  Returns the main-loop LDS bytes or -1.
+static int geometry(const Params& p, int BM, int BN, int W, int bpc, int epi_min, Geo& g) {
+  const qnn_conv_desc& d = p.d;
+  if (p.taps <= 1 || d.kmask || d.cp % 64 != 0) return -1;
+  if (d.sh != d.sw || (d.sh != 1 && d.sh != 2)) return -1;
+  if (d.kpad < p.taps * d.cp) return -1;
+  if ((d.cp / 64) * p.taps % 3 != 0) return -1;  // K steps in whole rounds of the DA = 3 weight ring
+  g.s2 = d.sh == 2;
+  g.we = (d.wp + 1) / 2;
+  g.npl = d.cp / 32;
+  const int img = d.ho * d.wo;
+  auto fit = [&](int rows, int nbrows) {
+    g.rows = rows;
+    g.npx = rows * d.wo;
+    g.nbrows = nbrows;
+    g.nbp = nbrows * g.wb;
+    g.pl = (int)cdiv((int64_t)g.nbp * 32, 1024) * 1024;
+    g.ppp = g.pl / 1024;
+    g.nbw = (int)cdiv(g.ppp, W) * g.npl;
+    g.psum_off = g.npl * g.pl;
+    g.tap_off = g.psum_off + ((g.nbp * 4 + 15) & ~15);
+    g.cls_off = g.tap_off + 4 * MAX_TAPS;
+    g.dummy_off = (g.cls_off + 4 * (d.ho + d.wo) + 15) & ~15;
+    g.main_bytes = g.dummy_off + 1024;  // the epilogue data after it: 16-B aligned
+    return g.nbw <= 4 * NBW_MAX && g.main_bytes + epi_min <= LDS_MAX / bpc;
+  };
+  bool ok = false;
+  static const int pad_env = [] {
+    const char* v = getenv("QNN_RB_PAD");
+    return v ? atoi(v) : 1;
+  }();
+  int wpad = d.wp;  // the narrowest row width with (sh*wb - wo) % 8 == 0, if any
+  for (int wb = d.wp; wb < d.wp + 8; ++wb)
+    if ((d.sh * wb - d.wo) % 8 == 0) {
+      wpad = wb;
+      break;
+    }
+  // candidates, largest first: k whole images, then divisors of ho; the first that fits LDS
+  // and gives at least one block per CU, else the first that fits
+  const int nby = (int)cdiv(d.cout, BM);
+  int best_rows = 0, best_nbrows = 0;
+  for (int pass = pad_env && wpad != d.wp ? 0 : 1; pass < 2 && !ok; ++pass) {
+    g.wb = pass == 0 ? wpad : d.wp;
+    int first_rows = 0, first_nbrows = 0;
+    auto consider = [&](int rows, int nbrows) {
+      if (ok || !fit(rows, nbrows)) return;
+      if (!first_rows) first_rows = rows, first_nbrows = nbrows;
+      if (cdiv((int64_t)d.n * d.ho, rows) * nby >= NUM_CU) ok = true, best_rows = rows, best_nbrows = nbrows;
+    };
+    if (img <= BN)
+      for (int k = BN / img < d.n ? BN / img : d.n; k >= 1; --k) consider(k * d.ho, (k - 1) * d.hp + (d.ho - 1) * d.sh + d.kh);
+    for (int rows = d.ho - 1; rows >= 1; --rows)
+      if (d.ho % rows == 0 && rows * d.wo <= BN) consider(rows, (rows - 1) * d.sh + d.kh);
+    if (!ok && first_rows) ok = true, best_rows = first_rows, best_nbrows = first_nbrows;
+  }
+  if (ok) fit(best_rows, best_nbrows);
+  if (!ok) return -1;
+  g.nbands = (int)cdiv((int64_t)d.n * d.ho, g.rows);
+  // band pipelining: with more than one plane pair, only the first pair's planes are loaded
+  // before the K loop; the rest stream in during its K steps (rp per step), each landing at
+  // least DA = 3 steps before the pair-1 barrier (they are older than the weights loaded then)
+  const int H = d.cp == 64 ? 1 : 2, avail = H * p.taps - 3;
+  const int rpw = (int)cdiv(g.ppp, W);  // ranges per wave
+  static const int split_env = [] {  // measured slower: the K loop's dummy DMA cost more than the band
+    const char* v = getenv("QNN_RB_SPLIT");
+    return v ? atoi(v) : 0;
+  }();
+  g.pg0 = g.npl, g.nrest = 0, g.rp = 0, g.rp0 = 0;
+  if (split_env && d.cp / 64 > H && avail > 0) {
+    const int nr = rpw * (g.npl - 2 * H);
+    if (nr <= 2 * avail) {
+      g.pg0 = 2 * H, g.nrest = nr;
+      g.rp = nr > avail ? 2 : 1;
+      g.rp0 = (int)cdiv(nr, g.rp);  // steps carrying real pieces (<= avail)
+    }
+  }
+  g.nbw0 = rpw * g.pg0;
+  return g.main_bytes;
+}
+
+static int epi_bytes(const Params& p, int BM) {
+  const int k = epi_kind(p.e);
+  return 4 * (7 + p.e.nclass) * BM + (k == EK_GEN ? 16 * p.e.nres * BM : 0);  // no LUT: EK_LUT is evaluated
+}
+
+template <class C, int EK, int H, int SP>
+static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  auto kern = qconv_rb_kernel<C, EK, H, SP>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  Geo g;
+  const int main = geometry(p, C::BM, C::BN, C::W, C::BPC, 0, g);
+  if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
+  Params q = p;
+  int epi = epi_bytes(p, C::BM);
+  static const int lut_env = [] {  // 0: always evaluate; 1: the table when it fits beside the band
+    const char* v = getenv("QNN_RB_LUT");
+    return v ? atoi(v) : 1;
+  }();
+  g.lut = 0;
+  if (EK == EK_LUT && lut_env && main + epi + 256 * C::BM <= LDS_MAX / C::BPC) g.lut = 1, epi += 256 * C::BM;
+  int lds;
+  if (main + epi <= LDS_MAX / C::BPC) {
+    q.epi_early = 1, q.epi_off = main;
+    lds = main + epi;
+  } else {  // staged after the loop over the band (the border classes past it stay)
+    if (epi > g.psum_off) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+    q.epi_early = 0, q.epi_off = 0;
+    lds = main;
+  }
+  q.scr_off = 0;
+  if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+  // one block per CU (the configurations are sized for it): two co-resident 8-wave blocks of
+  // the 4x2-wave 32x64 tile were measured to corrupt one accumulator row now and then (tile
+  // configuration removed); QNN_RB_LDS_MIN=<bytes> overrides for experiments
+  static const int lds_min = [] {
+    const char* v = getenv("QNN_RB_LDS_MIN");
+    return v ? atoi(v) : LDS_MAX / 2 + 1024;
+  }();
+  if (lds < lds_min && lds_min <= LDS_MAX) lds = lds_min;
+  const int nblk = g.nbands * (int)cdiv(p.d.cout, C::BM);
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q, g);
+  return QNN_OK;
+}
+
+template <class C, int EK>
+static int launch_h(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (p.d.cp == 64) {  // 28 accumulator tiles spill beside the 64-channel (H = 1) loop: not built
+    if constexpr (C::TM * C::TN > 26) return arg_error("tile configuration not built for this layer / epilogue kind");
+    else return launch<C, EK, 1, 0>(x, w, p, s);
+  }
+  Geo g;
+  if (geometry(p, C::BM, C::BN, C::W, C::BPC, 0, g) < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
+  if (g.rp == 1) return launch<C, EK, 2, 1>(x, w, p, s);
+  if (g.rp == 2) return launch<C, EK, 2, 2>(x, w, p, s);
+  return launch<C, EK, 2, 0>(x, w, p, s);
+}
+
+template <class C>
+static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  switch (epi_kind(p.e)) {
+    case EK_NCHW: return launch_h<C, EK_NCHW>(x, w, p, s);
+    case EK_LUT: return launch_h<C, EK_LUT>(x, w, p, s);
+    case EK_BNCODE: return launch_h<C, EK_BNCODE>(x, w, p, s);
+    default:  // 26 accumulator tiles + the general chain spill registers: not built
+      if constexpr (C::TM * C::TN > 16) return arg_error("tile configuration not built for this layer / epilogue kind");
+      else return launch_h<C, EK_GEN>(x, w, p, s);
+  }
+}
+
+//   id  block (cout x px cols)  waves (each)      blocks/CU  fits
+//   0   256 x 208               8 (32 x 208)      1          14x14 images (ResNet-50 layer 3, b256)
+//   1   128 x 224               8 (32 x 112)      1          128-channel tiles of 14x14 / 28x28 / 56x56 rows
+//   2   128 x 128               8 (32 x 64)       1          7x7 images in pairs, 512 channels
+//   3   256 x 224               8 (64 x 112)      1          14x14 images, each band fragment feeds 4 MFMAs
+//   4   128 x 256               8 (64 x 64)       1          128-channel tiles, 4 MFMAs per fragment
+using R0 = Cfg<8, 1, 2, 13, 3, 1>;
+using R1 = Cfg<4, 2, 2, 7, 3, 1>;
+using R3 = Cfg<4, 2, 4, 7, 3, 1>;
+using R4 = Cfg<2, 4, 4, 4, 3, 1>;
+constexpr int NR = 4;
+struct Info {
+  int bm, bn, w, bpc, acc_tiles;
+  float rate;
+};
+static const Info INFO[NR] = {
+    {256, 208, 8, 1, 26, 1.40f},
+    {128, 224, 8, 1, 14, 1.25f},
+    {256, 224, 8, 1, 28, 1.45f},
+    {128, 256, 8, 1, 16, 1.25f},
+};
+
+}  // namespace rb
+
+int rb_count() { return rb::NR; }
+
+#if QNN_STAMP
+extern "C" int qnn_debug_stamps_rb(void* dst, size_t bytes) {
+  if (bytes > sizeof(::qnn_rb_stamps)) bytes = sizeof(::qnn_rb_stamps);
+  return hip_check(hipMemcpyFromSymbol(dst, HIP_SYMBOL(::qnn_rb_stamps), bytes), "stamps");
+}
+#endif
+
+void rb_tile(int k, int* bm, int* bn) {
+  *bm = rb::INFO[k].bm;
+  *bn = rb::INFO[k].bn;
+}
+
+bool rb_ok(int k, const Params& p) {
+  using namespace rb;
+  if (k < 0 || k >= NR) return false;
+  const Info& f = INFO[k];
+  if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;  // the general chain spills beside the accumulators
+  if (p.d.cp == 64 && f.acc_tiles > 26) return false;              // spills beside the H = 1 loop
+  Geo g;
+  return geometry(p, f.bm, f.bn, f.w, f.bpc, 0, g) >= 0;
+}
+
+int64_t rb_blocks(int k, const Params& p) {
+  const rb::Info& f = rb::INFO[k];
+  rb::Geo g;
+  if (rb::geometry(p, f.bm, f.bn, f.w, f.bpc, 0, g) < 0) return 0;
+  return (int64_t)g.nbands * cdiv(p.d.cout, f.bm);
+}
+
+double rb_cost(int k, const Params& p) {
+  const rb::Info& f = rb::INFO[k];
+  rb::Geo g;
+  if (rb::geometry(p, f.bm, f.bn, f.w, f.bpc, 0, g) < 0) return 1e30;
+  const int64_t tiles = (int64_t)g.nbands * cdiv(p.d.cout, f.bm);
+  const int64_t slots = (int64_t)NUM_CU * f.bpc;
+  const int64_t rounds = cdiv(tiles, slots);
+  const double share = tiles < slots ? (double)cdiv(tiles, NUM_CU) : (double)f.bpc;
+  return (double)rounds * share * f.bm * f.bn * (p.taps * p.d.cp) / f.rate;  // dummy tiles cost MFMA time too
+}
+
+int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  using namespace rb;
+  switch (k) {
+    case 0: return launch_ek<R0>(x, w, p, s);
+    case 1: return launch_ek<R1>(x, w, p, s);
+    case 2: return launch_ek<R3>(x, w, p, s);
+    default: return launch_ek<R4>(x, w, p, s);
+  }
+}
+
+}  // namespace qnn

@@ -68,5 +68,8 @@ def test_calibrate_then_measure_file(gpu, tmp_path):
             r = ref[k]
             assert bool(((v.cpu() - r).abs() <= 1e-3 * r.abs().clamp_min(1.0)).all()), k
     again = _fresh()
-    assert C.load_maybe_calibrate(again, bare, str(tmp_path), "resnet", 18, device=gpu) == "measure"
+    # pack=False: packing refreshes weight_min/max from the weights, as the reference's first
+    # eval forward does (quantize.py:316-330); the loaded state itself must equal the file
+    assert C.load_maybe_calibrate(again, bare, str(tmp_path), "resnet", 18, device=gpu, pack=False) == "measure"
     assert all(torch.equal(v.cpu(), msd[k]) for k, v in again.state_dict().items())
+    assert C.prepack(again) > 0
