@@ -37,6 +37,10 @@
 #ifndef QNN_RB_ASM
 #define QNN_RB_ASM 1  // 1: band reads as inline asm with hand-counted lgkmcnt; 0: compiler-scheduled
 #endif
+#ifndef QNN_RB_ASM_A
+#define QNN_RB_ASM_A 0  // 1: weight loads as inline asm with hand-counted vmcnt (measured: no faster
+                        //    without the band stream, which measured slower itself); 0: compiler
+#endif
 #ifndef QNN_STAMP
 #define QNN_STAMP 0  // diagnostic builds only (make stamp_rb): per-wave s_memtime phase stamps
 #endif
@@ -239,9 +243,24 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       for (int i = 0; i < TM; ++i) dst[i] = (v4i){i, 1, 2, 3};
       return;
     }
-    const int kb = kbytes(cl);
+    const int8_t* base = wblk + kbytes(cl);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const v4i*>(wblk + kb + aoff[i]);
+    for (int i = 0; i < TM; ++i) {
+#if QNN_RB_ASM_A
+      // inline asm: the compiler's waitcnt pass loses count beside the LDS-DMA of the band
+      // stream (it drains vmcnt(0)); these loads are waited for by hand (wait_a below)
+      v4i r;
+      const uint64_t bu = (uint64_t)base;  // uniform: pin it to SGPRs for the saddr form
+      const uint64_t bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bu >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bu);
+      // s_nop 4: the saddr SGPRs may have just been written by v_readfirstlane, and a VMEM read
+      // of a VALU-written SGPR needs 5 wait states the compiler cannot see inside inline asm
+      asm volatile("s_nop 4\n\tglobal_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(aoff[i]), "s"((const int8_t*)bs));
+      dst[i] = r;
+#else
+      dst[i] = *reinterpret_cast<const v4i*>(base + aoff[i]);
+#endif
+    }
     if (H * cl.gp + cl.h < d.cp / 64 - 1 || cl.t < p.taps - 1 || cl.h < H - 1) advance(cl);  // clamp at the last step
   };
 #pragma unroll
@@ -278,6 +297,12 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   auto step = [&](auto slotc, auto dmac) {
     constexpr int SL = decltype(slotc)::value;
     constexpr bool DMA = decltype(dmac)::value;
+#if QNN_RB_ASM_A
+    // this step's weights were loaded DA-1 steps' worth of VMEM ago (SP band DMA + TM loads
+    // per step in the streaming phase; the first phase after it waits for more than needed)
+    wait_vmcnt<(DA - 1) * (TM + (DMA ? SP : 0))>();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const int dt = cc.tr * g.wb + (g.s2 ? (cc.tc & 1) * g.we + (cc.tc >> 1) : cc.tc);
     const int boff = (2 * (H * cc.gp + cc.h)) * g.pl + 32 * dt;
     v4i fb[TN];
@@ -332,6 +357,10 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   } else {
     run(KS, std::false_type{});
   }
+  // the clamped tail prefetch (asm loads the compiler cannot see) lands before any register
+  // it writes can be reused
+  wait_vmcnt<0>();
+  __builtin_amdgcn_sched_barrier(0);
 
 #if QNN_STAMP
   RB_TS(ts2);
@@ -420,7 +449,52 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       P.wo = P.ok ? cwo : lwo;
       pc = s_hc[P.ho] + s_hc[d.ho + P.wo];
     };
-    q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
+    const qnn_epilogue& e = p.e;
+    if (EK == EK_LUT && g.lut && c0 + BM <= d.cout && c0 + BM <= e.code0_cp) {
+      // fast path of the common case (a full channel tile, the code table staged): the
+      // epilogue_rb EK_LUT arithmetic with no per-group branch
+      const float* s_f = reinterpret_cast<const float*>(smem + p.epi_off);
+      const int8_t* s_lut = smem + p.epi_off + 4 * (7 + e.nclass) * BM;
+      const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+      const int gq = lane >> 4;
+      float4 sw[TM], bw[TM], bi[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cl = wm * 16 * TM + 16 * i + 4 * gq;
+        sw[i] = *reinterpret_cast<const float4*>(s_f + cl);
+        bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cl);
+        bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        q16::Pix P;
+        int pc;
+        pixel(j, P, pc);
+        int8_t* op = e.out_code0 + (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp + P.wo + e.code0_pad) *
+                                       e.code0_cp + c0 + wm * 16 * TM + 4 * gq;
+        const float* tp = s_f + (7 + pc) * BM + wm * 16 * TM + 4 * gq;
+        const f2 p2 = {(float)sumq[j], (float)sumq[j]};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float4 tb = *reinterpret_cast<const float4*>(tp + 16 * i);
+          const v4i& a = acc[i][j];
+          const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
+          const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
+                        (f2){bi[i].x, bi[i].y};
+          const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
+                        (f2){bi[i].z, bi[i].w};
+          const f2 q0 = qclamp2(v0, bnp) + MAGIC_U8, q1 = qclamp2(v1, bnp) + MAGIC_U8;
+          const int8_t* lp = s_lut + (wm * 16 * TM + 16 * i + 4 * gq) * 256;
+          const int b0 = (uint8_t)lp[__float_as_uint(q0.x) & 255u];
+          const int b1 = (uint8_t)lp[256 + (__float_as_uint(q0.y) & 255u)];
+          const int b2 = (uint8_t)lp[512 + (__float_as_uint(q1.x) & 255u)];
+          const int b3 = (uint8_t)lp[768 + (__float_as_uint(q1.y) & 255u)];
+          *reinterpret_cast<int*>(op + 16 * i) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        }
+      }
+    } else {
+      q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
+    }
   }
 #if QNN_STAMP
   RB_TS(ts6);
@@ -466,8 +540,8 @@ static int geometry(const Params& p, int BM, int BN, int W, int bpc, int epi_min
   };
   bool ok = false;
   static const int pad_env = [] {
-    const char* v = getenv("QNN_RB_PAD");
-    return v ? atoi(v) : 1;
+    const char* v = getenv("QNN_RB_PAD");  // measured: the staged code table beats conflict-free rows
+    return v ? atoi(v) : 0;
   }();
   int wpad = d.wp;  // the narrowest row width with (sh*wb - wo) % 8 == 0, if any
   for (int wb = d.wp; wb < d.wp + 8; ++wb)
