@@ -226,20 +226,31 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
   if (tp >= per_blk) return;  // c/8 not a divisor of 256: idle tail threads
   const int nxg = (wo + R - 1) / R, total = rows * nxg, cb = 8 * tc;
   if (blockIdx.x * per_blk + tp >= total) return;
-  float wv[K * K][8];
+  // every per-channel quantity as packed pairs (channels 2p, 2p+1): v_pk_fma/mul/add run the
+  // same IEEE fp32 op per element as the scalar form, so the results are bitwise unchanged
+  f2 wv[K * K][4];
 #pragma unroll
   for (int t = 0; t < K * K; ++t) {
     const float4 a = *reinterpret_cast<const float4*>(wt + t * c + cb);
     const float4 b = *reinterpret_cast<const float4*>(wt + t * c + cb + 4);
-    wv[t][0] = a.x, wv[t][1] = a.y, wv[t][2] = a.z, wv[t][3] = a.w;
-    wv[t][4] = b.x, wv[t][5] = b.y, wv[t][6] = b.z, wv[t][7] = b.w;
+    wv[t][0] = (f2){a.x, a.y}, wv[t][1] = (f2){a.z, a.w}, wv[t][2] = (f2){b.x, b.y}, wv[t][3] = (f2){b.z, b.w};
   }
-  float bi[8], mean[8], sq[8], wq[8], bq[8];
+  f2 bi[4], mean[4], sq[4], wq[4], bq[4];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    bi[u] = bias ? bias[cb + u] : 0.f;
-    if (has_bn) mean[u] = bn.mean[cb + u], sq[u] = bn.sq[cb + u], wq[u] = bn.wq[cb + u], bq[u] = bn.bq[cb + u];
+  for (int p = 0; p < 4; ++p) {
+    bi[p] = bias ? (f2){bias[cb + 2 * p], bias[cb + 2 * p + 1]} : (f2){0.f, 0.f};
+    if (has_bn) {
+      mean[p] = (f2){bn.mean[cb + 2 * p], bn.mean[cb + 2 * p + 1]};
+      sq[p] = (f2){bn.sq[cb + 2 * p], bn.sq[cb + 2 * p + 1]};
+      wq[p] = (f2){bn.wq[cb + 2 * p], bn.wq[cb + 2 * p + 1]};
+      bq[p] = (f2){bn.bq[cb + 2 * p], bn.bq[cb + 2 * p + 1]};
+    }
   }
+  const QParams bnp = make_qparams(bn.neg_min, bn.scale, bn.qmax);
+  const QParams c0p = make_qparams(c0.neg_min, c0.scale, c0.qmax);
+  const f2 xs2 = {x_scale, x_scale}, xm2 = {x_min, x_min};
+  const f2 bs2 = {bn.scale, bn.scale}, bm2 = {bn.min, bn.min};
+  (void)bn_inv, (void)c0_inv;
   // Every load unconditional (clamped in-buffer addresses: the padded buffer holds any row
   // oy*S + r and column < wp) and all K x NCOL issued together -- a load under a branch
   // gets its own vmcnt(0) wait.  Software-pipelined: the next group's loads are in flight
@@ -267,11 +278,11 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
     const int ox0 = xg * R;
     uint2 vn[K][NCOL];
     load(min(pg + step, total - 1), vn);
-    float acc[R][8];
+    f2 acc[R][4];
 #pragma unroll
     for (int j = 0; j < R; ++j)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc[j][u] = 0.f;
+      for (int p = 0; p < 4; ++p) acc[j][p] = (f2){0.f, 0.f};
 
 #pragma unroll
     for (int r = 0; r < K; ++r) {
@@ -282,18 +293,17 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
         const int px = ox0 * S + col;
         if (px < pad || px >= pad + w) continue;
         const uint32_t lo = v[r][col].x ^ 0x80808080u, hi = v[r][col].y ^ 0x80808080u;  // code' ^ 0x80 = code
-        float xh[8];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          xh[u] = dequant((float)((lo >> (8 * u)) & 255), x_scale, x_min);
-          xh[4 + u] = dequant((float)((hi >> (8 * u)) & 255), x_scale, x_min);
-        }
+        f2 xh[4];  // dequant(q) = q * s + min (quantize.py:100), pairs
+        xh[0] = (f2){(float)(lo & 255), (float)((lo >> 8) & 255)} * xs2 + xm2;
+        xh[1] = (f2){(float)((lo >> 16) & 255), (float)(lo >> 24)} * xs2 + xm2;
+        xh[2] = (f2){(float)(hi & 255), (float)((hi >> 8) & 255)} * xs2 + xm2;
+        xh[3] = (f2){(float)((hi >> 16) & 255), (float)(hi >> 24)} * xs2 + xm2;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
           const int s = col - j * S;
           if (s < 0 || s >= K) continue;  // compile-time
 #pragma unroll
-          for (int u = 0; u < 8; ++u) acc[j][u] = fmaf(xh[u], wv[r * K + s][u], acc[j][u]);
+          for (int p = 0; p < 4; ++p) acc[j][p] = pfma(xh[p], wv[r * K + s][p], acc[j][p]);
         }
       }
     }
@@ -302,32 +312,31 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
     for (int j = 0; j < R; ++j) {
       const int ox = ox0 + j;
       if (ox >= wo) break;
-      float val[8];
+      f2 val[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        float y = bias ? acc[j][u] + bi[u] : acc[j][u];
-        if (has_bn) {
-          const float q = quant_code_fast(y, bn.neg_min, bn.scale, bn_inv, bn.qmax);
-          float o = dequant(q, bn.scale, bn.min) - mean[u];  // bn_apply, quantize.py:488-499
-          o = o * sq[u];
-          o = o * wq[u];
-          y = o + bq[u];
+      for (int p = 0; p < 4; ++p) {
+        f2 y = bias ? acc[j][p] + bi[p] : acc[j][p];
+        if (has_bn) {  // bn_apply(quant_code(y)), quantize.py:488-499
+          f2 o = rint2(qclamp2(y, bnp)) * bs2;
+          o = o + bm2;
+          o = o - mean[p];
+          o = o * sq[p];
+          o = o * wq[p];
+          y = o + bq[p];
         }
-        val[u] = relu ? fmaxf(y, 0.f) : y;
+        if (relu) y.x = fmaxf(y.x, 0.f), y.y = fmaxf(y.y, 0.f);
+        val[p] = y;
       }
       if (out_f32) {
         float* o = out_f32 + (((size_t)img * ho + oy) * wo + ox) * c + cb;
-        *reinterpret_cast<float4*>(o) = make_float4(val[0], val[1], val[2], val[3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(val[4], val[5], val[6], val[7]);
+        *reinterpret_cast<float4*>(o) = make_float4(val[0].x, val[0].y, val[1].x, val[1].y);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(val[2].x, val[2].y, val[3].x, val[3].y);
       }
       if (c0.ptr) {
-        uint32_t p[2] = {0u, 0u};
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          p[u >> 2] |= (uint32_t)(((int)quant_code_fast(val[u], c0.neg_min, c0.scale, c0_inv, c0.qmax) - 128) & 255)
-                       << (8 * (u & 3));
+        const int p0 = pack4(qclamp2(val[0], c0p) + MAGIC_S8, qclamp2(val[1], c0p) + MAGIC_S8);
+        const int p1 = pack4(qclamp2(val[2], c0p) + MAGIC_S8, qclamp2(val[3], c0p) + MAGIC_S8);
         *reinterpret_cast<uint2*>(c0.ptr + (((size_t)img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * c0.cp + cb) =
-            make_uint2(p[0], p[1]);
+            make_uint2((uint32_t)p0, (uint32_t)p1);
       }
     }
 #pragma unroll
