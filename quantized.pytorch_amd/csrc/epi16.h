@@ -190,7 +190,9 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
     const int ptab = nparam + pc * BM;
     const f2 p2 = {(float)sumq[j], (float)sumq[j]};
     const int mc = P.m;  // a valid pixel (past-the-block slots hold the last one)
-    const int64_t px0 = (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp + P.wo + e.code0_pad) * e.code0_cp;
+    // padded pixel index (its factors < 2^24: full-rate 24-bit multiplies) x cp, 64-bit
+    const int64_t px0 = (int64_t)(__umul24(__umul24((unsigned)P.n, (unsigned)e.code0_hp) + (unsigned)(P.ho + e.code0_pad),
+                                           (unsigned)e.code0_wp) + (unsigned)(P.wo + e.code0_pad)) * e.code0_cp;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int cl = wm * 16 * TM + 16 * i + 4 * g;  // local channel of register 0

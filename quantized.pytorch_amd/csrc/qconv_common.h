@@ -143,5 +143,12 @@ bool rb_ok(int k, const Params& p);
 double rb_cost(int k, const Params& p);
 int64_t rb_blocks(int k, const Params& p);
 int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s);
+// qconv_direct.hip's short-K configurations (ids after the resident-band ones, through rb_*)
+int direct_count();
+void direct_tile(int k, int* bm, int* bn);
+bool direct_ok(int k, const Params& p);
+double direct_cost(int k, const Params& p);
+int64_t direct_blocks(int k, const Params& p);
+int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s);
 
 }  // namespace qnn

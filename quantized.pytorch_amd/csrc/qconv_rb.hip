@@ -687,7 +687,7 @@ static const Info INFO[NR] = {
 
 }  // namespace rb
 
-int rb_count() { return rb::NR; }
+int rb_count() { return rb::NR + direct_count(); }
 
 #if QNN_STAMP
 extern "C" int qnn_debug_stamps_rb(void* dst, size_t bytes) {
@@ -697,13 +697,15 @@ extern "C" int qnn_debug_stamps_rb(void* dst, size_t bytes) {
 #endif
 
 void rb_tile(int k, int* bm, int* bn) {
+  if (k >= rb::NR) return direct_tile(k - rb::NR, bm, bn);
   *bm = rb::INFO[k].bm;
   *bn = rb::INFO[k].bn;
 }
 
 bool rb_ok(int k, const Params& p) {
   using namespace rb;
-  if (k < 0 || k >= NR) return false;
+  if (k >= NR) return direct_ok(k - NR, p);
+  if (k < 0) return false;
   const Info& f = INFO[k];
   if (epi_kind(p.e) == EK_GEN && f.acc_tiles > 16) return false;  // the general chain spills beside the accumulators
   if (p.d.cp == 64 && f.acc_tiles > 26) return false;              // spills beside the H = 1 loop
@@ -712,6 +714,7 @@ bool rb_ok(int k, const Params& p) {
 }
 
 int64_t rb_blocks(int k, const Params& p) {
+  if (k >= rb::NR) return direct_blocks(k - rb::NR, p);
   const rb::Info& f = rb::INFO[k];
   rb::Geo g;
   if (rb::geometry(p, f.bm, f.bn, f.w, f.bpc, 0, g) < 0) return 0;
@@ -719,6 +722,7 @@ int64_t rb_blocks(int k, const Params& p) {
 }
 
 double rb_cost(int k, const Params& p) {
+  if (k >= rb::NR) return direct_cost(k - rb::NR, p);
   const rb::Info& f = rb::INFO[k];
   rb::Geo g;
   if (rb::geometry(p, f.bm, f.bn, f.w, f.bpc, 0, g) < 0) return 1e30;
@@ -731,6 +735,7 @@ double rb_cost(int k, const Params& p) {
 
 int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   using namespace rb;
+  if (k >= NR) return direct_launch(k - NR, x, w, p, s);
   switch (k) {
     case 0: return launch_ek<R0>(x, w, p, s);
     case 1: return launch_ek<R1>(x, w, p, s);

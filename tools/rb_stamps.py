@@ -87,7 +87,7 @@ def main():
     with torch.no_grad():
         eng()
     torch.cuda.synchronize()
-    tiles = a.tiles or list(range(_lib.CONV_TILES - 4, _lib.CONV_TILES))
+    tiles = a.tiles or [26, 27, 28, 29]
     seen = set()
     for idx, d, e in eng.convs:
         if d.kh != 3:
