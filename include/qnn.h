@@ -226,7 +226,7 @@ int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, 
  * LDS once per K chunk and every tap reads them at a shifted LDS address (no im2col
  * re-reads from L2); ids 26-29 the resident-band kernels (whole output rows per block, the
  * band of ALL input channels loaded once, weights streamed straight into registers, no
- * barrier in the K loop; kh x kw > 1, cp % 64 == 0); ids 30-31 the direct-fragment kernels for
+ * barrier in the K loop; kh x kw > 1, cp % 64 == 0); ids 30-32 the direct-fragment kernels for
  * short reductions (kpad <= 256: the space-to-depth stems, narrow 1x1s; every B fragment one
  * 16-byte load of one tap of one input pixel, persistent blocks).  An explicit tile that is
  * not built for the layer / epilogue kind is an argument error. */

@@ -25,14 +25,14 @@ namespace qnn {
 namespace dk {
 
 // 4 waves side by side along the pixels; each owns all TM 16-channel tiles of its TN
-// 16-pixel tiles.  CB channels per block; BM = 64 is the stride of the staged epilogue
+// 16-pixel tiles.  CB channels per block; BM = max(CB, 64) is the stride of the staged epilogue
 // vectors (stage_epi moves 64 floats per DMA; channels past the block's CB are staged, unused).
 // (WGM, BPC: the members stage_epi / epilogue_rb expect.)
 template <int TM_, int TN_>
 struct Cfg {
   static constexpr int WGM = 1, WGN = 4, TM = TM_, TN = TN_, BPC = 1;
   static constexpr int W = WGM * WGN, NT = 64 * W;
-  static constexpr int CB = TM * 16, BM = 64, BN = WGN * TN * 16;
+  static constexpr int CB = TM * 16, BM = CB < 64 ? 64 : CB, BN = WGN * TN * 16;
   static_assert(CB <= BM, "channel tile wider than the staging stride");
 };
 
@@ -224,14 +224,16 @@ static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStrea
 //   id  block (cout x px)   waves (each)       fits
 //   0   32 x 256            4 (32 x 64)        MobileNet's 32-channel stem, 32-channel 1x1s
 //   1   64 x 128            4 (64 x 32)        ResNet's 64-channel stem, 64-channel 1x1s
+//   2   128 x 64            4 (128 x 16)       128-channel 1x1s (MobileNet's pointwise layers)
 using D0 = Cfg<2, 4>;
 using D1 = Cfg<4, 2>;
-constexpr int ND = 2;
+using D2 = Cfg<8, 1>;
+constexpr int ND = 3;
 struct Info {
   int bm, bn, acc_tiles;
   float rate;
 };
-static const Info INFO[ND] = {{32, 256, 8, 1.0f}, {64, 128, 8, 1.0f}};
+static const Info INFO[ND] = {{32, 256, 8, 1.0f}, {64, 128, 8, 1.0f}, {128, 64, 8, 1.0f}};
 
 }  // namespace dk
 
@@ -247,7 +249,8 @@ bool direct_ok(int k, const Params& p) {
   const qnn_conv_desc& d = p.d;
   if (d.kpad > dk::KPAD_MAX || d.kpad % 64 || d.cp % 16 || d.cout % 16) return false;
   if (p.taps * d.cp > d.kpad || p.M >= (1 << 24)) return false;  // fdivmod's range
-  return dk::epi_bytes(p, 64) + 16 + 4 * (d.ho + d.wo) <= LDS_MAX;
+  const int bm = dk::INFO[k].bm < 64 ? 64 : dk::INFO[k].bm;
+  return dk::epi_bytes(p, bm) + 16 + 4 * (d.ho + d.wo) <= LDS_MAX;
 }
 
 int64_t direct_blocks(int k, const Params& p) {
@@ -270,7 +273,8 @@ int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipS
   if (!direct_ok(k, p)) return arg_error("tile configuration not built for this layer / epilogue kind");
   switch (k) {
     case 0: return dk::launch_ek<dk::D0>(x, w, p, s);
-    default: return dk::launch_ek<dk::D1>(x, w, p, s);
+    case 1: return dk::launch_ek<dk::D1>(x, w, p, s);
+    default: return dk::launch_ek<dk::D2>(x, w, p, s);
   }
 }
 
