@@ -48,7 +48,7 @@ __device__ __forceinline__ void fdivmod(int m, int D, float invD, int& q, int& r
 }
 
 template <class C, int EK, bool MASKED, int KS>
-__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(KS == 1 && C::TM == 2 && EK <= EK_LUT ? 4 : 1))) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+__global__ __launch_bounds__(C::NT) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                             const Params p) {
   constexpr int TM = C::TM, TN = C::TN, CB = C::CB, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
