@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 6
+#define QNN_ABI_VERSION 7
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -217,16 +217,25 @@ int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc
                     qnn_stream_t stream);
 
 /* Tile plan qnn_qconv2d_fwd would use for this layer (introspection for benchmarks and
- * profiles; no GPU work): configuration id, block tile (cout x pixels), grid size.
- * QNN_CONV_CFG=<id> in the environment forces a configuration. Any out pointer may be NULL. */
+ * profiles; no GPU work): configuration id, block tile (cout x pixels), and the number of
+ * block tiles (the persistent direct-fragment grid loops over them: qnn_conv_occupancy.grid
+ * is the launched grid).  Any out pointer may be NULL. */
 int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn, int* nblk);
+
+/* Launch resources of the configuration qnn_qconv2d_fwd would use (resident-band and
+ * direct-fragment configurations, ids >= 26): co-resident blocks per CU at its dynamic LDS
+ * (registers and LDS, hipOccupancyMaxActiveBlocksPerMultiprocessor), LDS bytes per block,
+ * and the launched grid.  No GPU work.  Any out pointer may be NULL. */
+int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* blocks_per_cu,
+                       int* lds_bytes, int* grid);
 
 /* Number of tile configurations (valid qnn_conv_desc.tile values are 1 .. count).  Those with
  * ids 12-25 are the halo-band kernels for kh x kw > 1: the block's input rows are read into
  * LDS once per K chunk and every tap reads them at a shifted LDS address (no im2col
- * re-reads from L2); ids 26-29 the resident-band kernels (whole output rows per block, the
+ * re-reads from L2); ids 26-30 the resident-band kernels (whole output rows per block, the
  * band of ALL input channels loaded once, weights streamed straight into registers, no
- * barrier in the K loop; kh x kw > 1, cp % 64 == 0); ids 30-32 the direct-fragment kernels for
+ * barrier in the K loop; kh x kw > 1, cp % 64 == 0; id 30 runs two blocks per CU); ids 31-33
+ * the direct-fragment kernels for
  * short reductions (kpad <= 256: the space-to-depth stems, narrow 1x1s; every B fragment one
  * 16-byte load of one tap of one input pixel, persistent blocks).  An explicit tile that is
  * not built for the layer / epilogue kind is an argument error. */

@@ -210,8 +210,12 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
           float* yp = e.out_f32 + ((int64_t)P.n * d.cout + c) * HoWo + P.ho * d.wo + P.wo;
           const float y4[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+          for (int r = 0; r < 4; ++r) {
             if (c + r < d.cout) yp[(int64_t)r * HoWo] = y4[r];
+#if QNN_RB_STORE_WAIT  // diagnostic build: every store has read its operands before the next instruction
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+          }
         }
         continue;
       }

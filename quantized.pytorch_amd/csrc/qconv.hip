@@ -1482,12 +1482,14 @@ static double cfg_cost(int k, const Params& p) {
 }
 
 static int pick_cfg(const Params& p) {
-  static int forced = [] {
+  auto ok = [&](int k) { return cfg_ok(k, p); };
+#if QNN_STAMP || QNN_ABLATE
+  static int forced = [] {  // diagnostic builds only: QNN_CONV_CFG overrides every caller
     const char* v = getenv("QNN_CONV_CFG");
     return v ? atoi(v) : -1;
   }();
-  auto ok = [&](int k) { return cfg_ok(k, p); };
-  if (ok(forced)) return forced;  // QNN_CONV_CFG: experiments override every caller
+  if (ok(forced)) return forced;
+#endif
   if (p.d.tile > 0) return ok(p.d.tile - 1) ? p.d.tile - 1 : -1;  // explicit: built, or an argument error
   int best = -1;
   double bc = 0;
@@ -1562,11 +1564,15 @@ static int conv_params(const qnn_conv_desc& d, const qnn_epilogue& e, Params& p)
   p.lgcpt = __builtin_ctz(d.cp / 16);
   p.kw_magic = (65536 + d.kw - 1) / d.kw;
   p.ct = (int)cdiv(d.cout, 32);
-  static const int stagger = [] {
+#if QNN_STAMP || QNN_ABLATE
+  static const int stagger = [] {  // diagnostic builds only: QNN_CONV_STAGGER=0 disables
     const char* v = getenv("QNN_CONV_STAGGER");
     return v ? atoi(v) : 1;
   }();
   p.stagger = stagger;
+#else
+  p.stagger = 1;
+#endif
   return QNN_OK;
 }
 
@@ -1588,6 +1594,25 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
   if (nblk) *nblk = k >= rb_first() ? (int)rb_blocks(k - rb_first(), p) : (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm));
+  return QNN_OK;
+}
+
+extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* blocks_per_cu,
+                                  int* lds_bytes, int* grid) {
+  QNN_REQUIRE(desc && epi, "null descriptor");
+  Params p;
+  const int rc = conv_params(*desc, *epi, p);
+  if (rc != QNN_OK) return rc;
+  const int k = pick_cfg(p);
+  QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
+  QNN_REQUIRE(k >= rb_first(), "occupancy is reported for the resident-band and direct-fragment configurations");
+  Occ o{0, 0, 0};
+  const int r = rb_launch(k - rb_first(), nullptr, nullptr, p, nullptr, &o);
+  if (r != QNN_OK) return r;
+  if (cfg) *cfg = k;
+  if (blocks_per_cu) *blocks_per_cu = o.blocks_per_cu;
+  if (lds_bytes) *lds_bytes = o.lds;
+  if (grid) *grid = o.grid;
   return QNN_OK;
 }
 

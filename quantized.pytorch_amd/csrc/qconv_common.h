@@ -130,6 +130,14 @@ __device__ __forceinline__ void stage_epi(const Params& p, const int8_t* x, int8
   }
 }
 
+// Launch resources of one configuration (qnn_conv_occupancy): when a launch function is given
+// an Occ it fills it and returns without launching.
+struct Occ {
+  int blocks_per_cu;  // co-resident blocks per CU at the launch's LDS (hipOccupancy...)
+  int lds;            // dynamic LDS bytes per block
+  int grid;           // blocks launched
+};
+
 // qconv16.hip's configurations (ids NCFG.. of qnn_conv_plan): count, tile, availability, cost, launch
 int q16_count();
 void q16_tile(int k, int* bm, int* bn);
@@ -142,13 +150,13 @@ void rb_tile(int k, int* bm, int* bn);
 bool rb_ok(int k, const Params& p);
 double rb_cost(int k, const Params& p);
 int64_t rb_blocks(int k, const Params& p);
-int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s);
+int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
 // qconv_direct.hip's short-K configurations (ids after the resident-band ones, through rb_*)
 int direct_count();
 void direct_tile(int k, int* bm, int* bn);
 bool direct_ok(int k, const Params& p);
 double direct_cost(int k, const Params& p);
 int64_t direct_blocks(int k, const Params& p);
-int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s);
+int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
 
 }  // namespace qnn

@@ -16,7 +16,9 @@
 // * The block's CB channels are all of a small cout (32 or 64): no wasted MFMA rows, and the
 //   epilogue (q16::epilogue_rb: registers-resident channel parameters, LDS code table) is
 //   spread over 4 waves x TN 16-pixel tiles with several blocks resident per CU.
-#include <stdlib.h>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "qconv_common.h"
 #include "epi16.h"
@@ -168,8 +170,33 @@ static int epi_bytes(const Params& p, int BM) {
   return 4 * (7 + p.e.nclass) * BM + (k == EK_GEN ? 16 * p.e.nres * BM : 0) + (k == EK_LUT ? 256 * BM : 0);
 }
 
+// Co-resident blocks per CU of one kernel at `lds` bytes, queried once per (kernel, lds).  The
+// cache is shared by every layer and caller thread (the ABI is re-entrant per stream; the
+// reference's DataParallel runs replica forwards from threads, main.py:345), so it is locked.
+static int blocks_per_cu(const void* kern, int nt, int lds) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(kern, lds);
+  const auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nt, lds) != hipSuccess || n < 1) n = 1;
+  cache.emplace(key, n);
+  return n;
+}
+
+// The persistent grid: as many blocks as fit at once, a whole number per channel tile
+template <class C>
+static int64_t persistent_grid(const Params& p, int per_cu) {
+  const int64_t nby = cdiv(p.d.cout, C::CB), tiles = cdiv(p.M, C::BN) * nby;
+  int64_t nblk = ((int64_t)NUM_CU * per_cu / nby) * nby;
+  nblk = nblk < nby ? nby : nblk;
+  return nblk < tiles ? nblk : tiles;
+}
+
 template <class C, int EK, bool MASKED, int KS>
-static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   auto kern = qconv_direct_kernel<C, EK, MASKED, KS>;
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
@@ -179,45 +206,40 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
   if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
   Params q = p;
   q.epi_off = 0, q.epi_early = 1, q.scr_off = epi;
-  // persistent grid: as many blocks as fit at once, a whole number per channel tile
-  static int per_cu = -1;
-  static int per_cu_lds = -1;
-  if (per_cu < 0 || per_cu_lds != lds) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, C::NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    per_cu_lds = lds;
+  const int per_cu = blocks_per_cu((const void*)kern, C::NT, lds);
+  const int64_t nblk = persistent_grid<C>(p, per_cu);
+  if (occ) {
+    occ->blocks_per_cu = per_cu, occ->lds = lds, occ->grid = (int)nblk;
+    return QNN_OK;
   }
-  const int64_t nby = cdiv(p.d.cout, C::CB), tiles = cdiv(p.M, C::BN) * nby;
-  int64_t nblk = ((int64_t)NUM_CU * per_cu / nby) * nby;
-  nblk = nblk < nby ? nby : nblk;
-  nblk = nblk < tiles ? nblk : tiles;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(C::NT), lds, s, x, w, q);
   return QNN_OK;
 }
 
 template <class C, int EK, bool MASKED>
-static int launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+static int launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   switch ((p.taps * (p.d.cp >> 4) + 3) >> 2) {  // K steps holding real chunks
-    case 1: return launch<C, EK, MASKED, 1>(x, w, p, s);
-    case 2: return launch<C, EK, MASKED, 2>(x, w, p, s);
-    case 3: return launch<C, EK, MASKED, 3>(x, w, p, s);
-    default: return launch<C, EK, MASKED, 4>(x, w, p, s);
+    case 1: return launch<C, EK, MASKED, 1>(x, w, p, s, occ);
+    case 2: return launch<C, EK, MASKED, 2>(x, w, p, s, occ);
+    case 3: return launch<C, EK, MASKED, 3>(x, w, p, s, occ);
+    default: return launch<C, EK, MASKED, 4>(x, w, p, s, occ);
   }
 }
 
 template <class C, int EK>
-static int launch_m(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  return p.d.kmask ? launch_k<C, EK, true>(x, w, p, s) : launch_k<C, EK, false>(x, w, p, s);
+static int launch_m(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  return p.d.kmask ? launch_k<C, EK, true>(x, w, p, s, occ) : launch_k<C, EK, false>(x, w, p, s, occ);
 }
 
 template <class C>
-static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return launch_m<C, EK_NCHW>(x, w, p, s);
-    case EK_LUT: return launch_m<C, EK_LUT>(x, w, p, s);
-    case EK_BNCODE: return launch_m<C, EK_BNCODE>(x, w, p, s);
+    case EK_NCHW: return launch_m<C, EK_NCHW>(x, w, p, s, occ);
+    case EK_LUT: return launch_m<C, EK_LUT>(x, w, p, s, occ);
+    case EK_BNCODE: return launch_m<C, EK_BNCODE>(x, w, p, s, occ);
     default:  // the general chain spills beside more than 16 accumulator tiles: not built
       if constexpr (C::TM * C::TN > 16) return arg_error("tile configuration not built for this layer / epilogue kind");
-      else return launch_m<C, EK_GEN>(x, w, p, s);
+      else return launch_m<C, EK_GEN>(x, w, p, s, occ);
   }
 }
 
@@ -253,6 +275,7 @@ bool direct_ok(int k, const Params& p) {
   return dk::epi_bytes(p, bm) + 16 + 4 * (d.ho + d.wo) <= LDS_MAX;
 }
 
+// pixel tiles x channel tiles (the persistent grid loops over them: qnn_conv_occupancy.grid)
 int64_t direct_blocks(int k, const Params& p) {
   const dk::Info& f = dk::INFO[k];
   return cdiv(p.M, f.bn) * cdiv(p.d.cout, f.bm);
@@ -269,12 +292,12 @@ double direct_cost(int k, const Params& p) {
   return (double)rounds * share * f.bm * f.bn * p.d.kpad / f.rate;
 }
 
-int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   if (!direct_ok(k, p)) return arg_error("tile configuration not built for this layer / epilogue kind");
   switch (k) {
-    case 0: return dk::launch_ek<dk::D0>(x, w, p, s);
-    case 1: return dk::launch_ek<dk::D1>(x, w, p, s);
-    default: return dk::launch_ek<dk::D2>(x, w, p, s);
+    case 0: return dk::launch_ek<dk::D0>(x, w, p, s, occ);
+    case 1: return dk::launch_ek<dk::D1>(x, w, p, s, occ);
+    default: return dk::launch_ek<dk::D2>(x, w, p, s, occ);
   }
 }
 

@@ -37,10 +37,6 @@
 #ifndef QNN_RB_ASM
 #define QNN_RB_ASM 1  // 1: band reads as inline asm with hand-counted lgkmcnt; 0: compiler-scheduled
 #endif
-#ifndef QNN_RB_ASM_A
-#define QNN_RB_ASM_A 0  // 1: weight loads as inline asm with hand-counted vmcnt (measured: no faster
-                        //    without the band stream, which measured slower itself); 0: compiler
-#endif
 #ifndef QNN_STAMP
 #define QNN_STAMP 0  // diagnostic builds only (make stamp_rb): per-wave s_memtime phase stamps
 #endif
@@ -96,18 +92,12 @@ struct Geo {
   int npx;        // output pixels per block (rows * wo)
   int nbands;     // blocks along the pixels
   int nbrows;     // padded input rows of a band
-  int wb, we, s2; // band row width (>= wp, padded so (sh*wb - wo) % 8 == 0 when LDS allows: a 16-pixel
-                  // tile straddling an output row then keeps its 16 distinct bank slots);
-                  // stride 2: even columns first, we = (wp + 1) / 2
+  int wb, we, s2; // band row width (= wp); stride 2: even columns first, we = (wp + 1) / 2
   int nbp;        // band pixels (nbrows * wb)
   int pl;         // bytes per 32-byte plane (1 KiB multiple)
   int npl;        // planes (cp / 32)
   int ppp;        // 1 KiB DMA pieces per plane
   int nbw;        // band DMA pieces per wave
-  int pg0, nbw0;  // planes of group 0 (the first plane pair's, or all) and its DMA per wave
-  int nrest;      // later pieces per wave, issued in the first rp0 K steps (kernel SP per step,
-  int rp, rp0;    //   the u-th at rest index step + u*rp0); rp = SP (0: no split)
-  int dummy_off;  // LDS: the KiB the dummy DMA land in
   int lut;        // EK_LUT: the 256-byte-per-channel code table is staged (else evaluated)
   int psum_off;   // LDS: int channel sum of each band pixel
   int tap_off;    // LDS: int band offset (pixels) of each tap
@@ -116,10 +106,9 @@ struct Geo {
 };
 
 // ---------------------------------------------------------------- kernel
-// SP: band pieces issued per K step (0: the whole band before the loop; 1 or 2: the first
-// plane pair's planes before it, the rest SP per step, every step issuing exactly SP DMA --
-// dummies past the rest -- so every weight wait stays a compile-time vmcnt)
-template <class C, int EK, int H, int SP>
+// The whole band lands before the K loop (one vmcnt(0) + barrier); the weights are plain
+// compiler-scheduled loads, so every VMEM wait in the loop is the compiler's own.
+template <class C, int EK, int H>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_rb_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
   constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
@@ -171,30 +160,13 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     asm volatile("" : "+v"(off));
     __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)band_dst(r, v), 16, 0, 0);
   };
-  // group 0 (planes [0, pg0): the first plane pair's, or all) now
-  for (int k = 0; k < g.nbw0; ++k) issue_piece(wave + W * (k / g.pg0), k % g.pg0);
+  for (int k = 0; k < g.nbw; ++k) issue_piece(wave + W * (k / g.npl), k % g.npl);
   // the epilogue's data next (EK_LUT: with its code table when g.lut, else evaluated)
   auto stage = [&] {
     if (EK == EK_LUT && g.lut) stage_epi<C, EK_LUT>(p, x, smem + p.epi_off, c0, wave, lane);
     else stage_epi<C, (EK == EK_LUT ? EK_BNCODE : EK)>(p, x, smem + p.epi_off, c0, wave, lane);
   };
   if (p.epi_early) stage();
-  auto issue_rest = [&](int s) {  // branch-free: exactly SP DMA
-    const int pr = g.npl - g.pg0;     // planes of the rest
-#pragma unroll
-    for (int u = 0; u < SP; ++u) {
-      const int k = s + u * g.rp0;  // this wave's u-th rest piece of step s
-      const bool real = s < g.rp0 && k < g.nrest;
-      int r = wave + W * (k / pr);
-      r = r < g.ppp ? r : g.ppp - 1;
-      const int v = g.pg0 + k % pr;
-      uint32_t off = band_src(r, v);
-      off = real ? off : (uint32_t)d.zero_off;  // dummies: the zero page into the dummy KiB
-      asm volatile("" : "+v"(off));
-      int8_t* dst = real ? band_dst(r, v) : smem + g.dummy_off;
-      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)dst, 16, 0, 0);
-    }
-  };
 
   // ---- this lane's pixels: block pixel q = (wn*TN + j)*16 + (lane & 15); past the block
   // (or the batch) they stand in for the block's last pixel and are never stored
@@ -245,22 +217,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     }
     const int8_t* base = wblk + kbytes(cl);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#if QNN_RB_ASM_A
-      // inline asm: the compiler's waitcnt pass loses count beside the LDS-DMA of the band
-      // stream (it drains vmcnt(0)); these loads are waited for by hand (wait_a below)
-      v4i r;
-      const uint64_t bu = (uint64_t)base;  // uniform: pin it to SGPRs for the saddr form
-      const uint64_t bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bu >> 32)) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bu);
-      // s_nop 4: the saddr SGPRs may have just been written by v_readfirstlane, and a VMEM read
-      // of a VALU-written SGPR needs 5 wait states the compiler cannot see inside inline asm
-      asm volatile("s_nop 4\n\tglobal_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(aoff[i]), "s"((const int8_t*)bs));
-      dst[i] = r;
-#else
-      dst[i] = *reinterpret_cast<const v4i*>(base + aoff[i]);
-#endif
-    }
+    for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const v4i*>(base + aoff[i]);
     if (H * cl.gp + cl.h < d.cp / 64 - 1 || cl.t < p.taps - 1 || cl.h < H - 1) advance(cl);  // clamp at the last step
   };
 #pragma unroll
@@ -289,20 +246,12 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
 #endif
 
   Cur cc = {0, 0, 0, 0, 0};
-  int ks = 0;  // K steps done
   // One K step: the TN band fragments are read up front (inline asm, so the compiler
   // cannot interleave each read with its first use), then each fragment's TM MFMAs wait
   // only for that fragment (LDS returns in order: lgkmcnt(TN-1-j)).  The partner wave on
   // the SIMD runs its MFMAs while this one waits for its reads.
-  auto step = [&](auto slotc, auto dmac) {
+  auto step = [&](auto slotc) {
     constexpr int SL = decltype(slotc)::value;
-    constexpr bool DMA = decltype(dmac)::value;
-#if QNN_RB_ASM_A
-    // this step's weights were loaded DA-1 steps' worth of VMEM ago (SP band DMA + TM loads
-    // per step in the streaming phase; the first phase after it waits for more than needed)
-    wait_vmcnt<(DA - 1) * (TM + (DMA ? SP : 0))>();
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     const int dt = cc.tr * g.wb + (g.s2 ? (cc.tc & 1) * g.we + (cc.tc >> 1) : cc.tc);
     const int boff = (2 * (H * cc.gp + cc.h)) * g.pl + 32 * dt;
     v4i fb[TN];
@@ -334,33 +283,16 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
         }
       }
     });
-    if constexpr (DMA) issue_rest(ks);  // older than the weights loaded next: landed DA steps later
     load_a(fa[SL]);
     advance(cc);
-    ++ks;
   };
-  auto run = [&](int nsteps, auto dmac) {
 #pragma nounroll
-    for (int k0 = 0; k0 < nsteps; k0 += DA) {
-      step(std::integral_constant<int, 0>{}, dmac);
-      if constexpr (DA > 1) step(std::integral_constant<int, 1>{}, dmac);
-      if constexpr (DA > 2) step(std::integral_constant<int, 2>{}, dmac);
-      if constexpr (DA > 3) step(std::integral_constant<int, 3>{}, dmac);
-    }
-  };
-  if constexpr (SP > 0) {
-    // plane pair 0 with the rest of the band streaming in, then every wave's rest has landed
-    run(H * p.taps, std::true_type{});
-    wait_vmcnt<DA*(TM + SP)>();
-    __syncthreads();
-    run(KS - H * p.taps, std::false_type{});
-  } else {
-    run(KS, std::false_type{});
+  for (int k0 = 0; k0 < KS; k0 += DA) {
+    step(std::integral_constant<int, 0>{});
+    if constexpr (DA > 1) step(std::integral_constant<int, 1>{});
+    if constexpr (DA > 2) step(std::integral_constant<int, 2>{});
+    if constexpr (DA > 3) step(std::integral_constant<int, 3>{});
   }
-  // the clamped tail prefetch (asm loads the compiler cannot see) lands before any register
-  // it writes can be reused
-  wait_vmcnt<0>();
-  __builtin_amdgcn_sched_barrier(0);
 
 #if QNN_STAMP
   RB_TS(ts2);
@@ -534,27 +466,16 @@ static int geometry(const Params& p, int BM, int BN, int W, int bpc, int epi_min
     g.psum_off = g.npl * g.pl;
     g.tap_off = g.psum_off + ((g.nbp * 4 + 15) & ~15);
     g.cls_off = g.tap_off + 4 * MAX_TAPS;
-    g.dummy_off = (g.cls_off + 4 * (d.ho + d.wo) + 15) & ~15;
-    g.main_bytes = g.dummy_off + 1024;  // the epilogue data after it: 16-B aligned
+    g.main_bytes = (g.cls_off + 4 * (d.ho + d.wo) + 15) & ~15;  // the epilogue data after it: 16-B aligned
     return g.nbw <= 4 * NBW_MAX && g.main_bytes + epi_min <= LDS_MAX / bpc;
   };
   bool ok = false;
-  static const int pad_env = [] {
-    const char* v = getenv("QNN_RB_PAD");  // measured: the staged code table beats conflict-free rows
-    return v ? atoi(v) : 0;
-  }();
-  int wpad = d.wp;  // the narrowest row width with (sh*wb - wo) % 8 == 0, if any
-  for (int wb = d.wp; wb < d.wp + 8; ++wb)
-    if ((d.sh * wb - d.wo) % 8 == 0) {
-      wpad = wb;
-      break;
-    }
   // candidates, largest first: k whole images, then divisors of ho; the first that fits LDS
   // and gives at least one block per CU, else the first that fits
   const int nby = (int)cdiv(d.cout, BM);
   int best_rows = 0, best_nbrows = 0;
-  for (int pass = pad_env && wpad != d.wp ? 0 : 1; pass < 2 && !ok; ++pass) {
-    g.wb = pass == 0 ? wpad : d.wp;
+  g.wb = d.wp;
+  {
     int first_rows = 0, first_nbrows = 0;
     auto consider = [&](int rows, int nbrows) {
       if (ok || !fit(rows, nbrows)) return;
@@ -570,25 +491,6 @@ static int geometry(const Params& p, int BM, int BN, int W, int bpc, int epi_min
   if (ok) fit(best_rows, best_nbrows);
   if (!ok) return -1;
   g.nbands = (int)cdiv((int64_t)d.n * d.ho, g.rows);
-  // band pipelining: with more than one plane pair, only the first pair's planes are loaded
-  // before the K loop; the rest stream in during its K steps (rp per step), each landing at
-  // least DA = 3 steps before the pair-1 barrier (they are older than the weights loaded then)
-  const int H = d.cp == 64 ? 1 : 2, avail = H * p.taps - 3;
-  const int rpw = (int)cdiv(g.ppp, W);  // ranges per wave
-  static const int split_env = [] {  // measured slower: the K loop's dummy DMA cost more than the band
-    const char* v = getenv("QNN_RB_SPLIT");
-    return v ? atoi(v) : 0;
-  }();
-  g.pg0 = g.npl, g.nrest = 0, g.rp = 0, g.rp0 = 0;
-  if (split_env && d.cp / 64 > H && avail > 0) {
-    const int nr = rpw * (g.npl - 2 * H);
-    if (nr <= 2 * avail) {
-      g.pg0 = 2 * H, g.nrest = nr;
-      g.rp = nr > avail ? 2 : 1;
-      g.rp0 = (int)cdiv(nr, g.rp);  // steps carrying real pieces (<= avail)
-    }
-  }
-  g.nbw0 = rpw * g.pg0;
   return g.main_bytes;
 }
 
@@ -597,23 +499,16 @@ static int epi_bytes(const Params& p, int BM) {
   return 4 * (7 + p.e.nclass) * BM + (k == EK_GEN ? 16 * p.e.nres * BM : 0);  // no LUT: EK_LUT is evaluated
 }
 
-template <class C, int EK, int H, int SP>
-static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  auto kern = qconv_rb_kernel<C, EK, H, SP>;
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
-  Geo g;
+// LDS bytes of one block and the Params/Geo it runs with, or a negative status
+template <class C, int EK>
+static int plan_lds(const Params& p, Params& q, Geo& g) {
   const int main = geometry(p, C::BM, C::BN, C::W, C::BPC, 0, g);
   if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
-  Params q = p;
+  q = p;
   int epi = epi_bytes(p, C::BM);
-  static const int lut_env = [] {  // 0: always evaluate; 1: the table when it fits beside the band
-    const char* v = getenv("QNN_RB_LUT");
-    return v ? atoi(v) : 1;
-  }();
+  // EK_LUT: the 256-byte-per-channel code table beside the band when it fits (else evaluated)
   g.lut = 0;
-  if (EK == EK_LUT && lut_env && main + epi + 256 * C::BM <= LDS_MAX / C::BPC) g.lut = 1, epi += 256 * C::BM;
+  if (EK == EK_LUT && main + epi + 256 * C::BM <= LDS_MAX / C::BPC) g.lut = 1, epi += 256 * C::BM;
   int lds;
   if (main + epi <= LDS_MAX / C::BPC) {
     q.epi_early = 1, q.epi_off = main;
@@ -625,55 +520,65 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
   }
   q.scr_off = 0;
   if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
-  // one block per CU (the configurations are sized for it): two co-resident 8-wave blocks of
-  // the 4x2-wave 32x64 tile were measured to corrupt one accumulator row now and then (tile
-  // configuration removed); QNN_RB_LDS_MIN=<bytes> overrides for experiments
-  static const int lds_min = [] {
-    const char* v = getenv("QNN_RB_LDS_MIN");
-    return v ? atoi(v) : LDS_MAX / 2 + 1024;
-  }();
-  if (lds < lds_min && lds_min <= LDS_MAX) lds = lds_min;
+  return lds;
+}
+
+template <class C, int EK, int H>
+static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  auto kern = qconv_rb_kernel<C, EK, H>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  Geo g;
+  Params q;
+  const int lds = plan_lds<C, EK>(p, q, g);
+  if (lds < 0) return lds;
+  // natural occupancy: as many blocks per CU as registers and LDS allow
   const int nblk = g.nbands * (int)cdiv(p.d.cout, C::BM);
+  if (occ) {
+    int n = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, C::NT, lds);
+    if (e != hipSuccess) return hip_check(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    occ->blocks_per_cu = n, occ->lds = lds, occ->grid = nblk;
+    return QNN_OK;
+  }
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q, g);
   return QNN_OK;
 }
 
 template <class C, int EK>
-static int launch_h(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+static int launch_h(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   if (p.d.cp == 64) {  // 28 accumulator tiles spill beside the 64-channel (H = 1) loop: not built
     if constexpr (C::TM * C::TN > 26) return arg_error("tile configuration not built for this layer / epilogue kind");
-    else return launch<C, EK, 1, 0>(x, w, p, s);
+    else return launch<C, EK, 1>(x, w, p, s, occ);
   }
-  Geo g;
-  if (geometry(p, C::BM, C::BN, C::W, C::BPC, 0, g) < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
-  if (g.rp == 1) return launch<C, EK, 2, 1>(x, w, p, s);
-  if (g.rp == 2) return launch<C, EK, 2, 2>(x, w, p, s);
-  return launch<C, EK, 2, 0>(x, w, p, s);
+  return launch<C, EK, 2>(x, w, p, s, occ);
 }
 
 template <class C>
-static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return launch_h<C, EK_NCHW>(x, w, p, s);
-    case EK_LUT: return launch_h<C, EK_LUT>(x, w, p, s);
-    case EK_BNCODE: return launch_h<C, EK_BNCODE>(x, w, p, s);
+    case EK_NCHW: return launch_h<C, EK_NCHW>(x, w, p, s, occ);
+    case EK_LUT: return launch_h<C, EK_LUT>(x, w, p, s, occ);
+    case EK_BNCODE: return launch_h<C, EK_BNCODE>(x, w, p, s, occ);
     default:  // 26 accumulator tiles + the general chain spill registers: not built
       if constexpr (C::TM * C::TN > 16) return arg_error("tile configuration not built for this layer / epilogue kind");
-      else return launch_h<C, EK_GEN>(x, w, p, s);
+      else return launch_h<C, EK_GEN>(x, w, p, s, occ);
   }
 }
 
 //   id  block (cout x px cols)  waves (each)      blocks/CU  fits
 //   0   256 x 208               8 (32 x 208)      1          14x14 images (ResNet-50 layer 3, b256)
 //   1   128 x 224               8 (32 x 112)      1          128-channel tiles of 14x14 / 28x28 / 56x56 rows
-//   2   128 x 128               8 (32 x 64)       1          7x7 images in pairs, 512 channels
-//   3   256 x 224               8 (64 x 112)      1          14x14 images, each band fragment feeds 4 MFMAs
-//   4   128 x 256               8 (64 x 64)       1          128-channel tiles, 4 MFMAs per fragment
+//   2   256 x 224               8 (64 x 112)      1          14x14 images, each band fragment feeds 4 MFMAs
+//   3   128 x 256               8 (64 x 64)       1          128-channel tiles, 4 MFMAs per fragment
+//   4   128 x 128               8 (32 x 64)       2          two co-resident blocks (<= 128 VGPRs, <= 80 KiB LDS)
 using R0 = Cfg<8, 1, 2, 13, 3, 1>;
 using R1 = Cfg<4, 2, 2, 7, 3, 1>;
 using R3 = Cfg<4, 2, 4, 7, 3, 1>;
 using R4 = Cfg<2, 4, 4, 4, 3, 1>;
-constexpr int NR = 4;
+using R5 = Cfg<4, 2, 2, 4, 3, 2>;
+constexpr int NR = 5;
 struct Info {
   int bm, bn, w, bpc, acc_tiles;
   float rate;
@@ -683,6 +588,7 @@ static const Info INFO[NR] = {
     {128, 224, 8, 1, 14, 1.25f},
     {256, 224, 8, 1, 28, 1.45f},
     {128, 256, 8, 1, 16, 1.25f},
+    {128, 128, 8, 2, 8, 0.60f},
 };
 
 }  // namespace rb
@@ -733,14 +639,15 @@ double rb_cost(int k, const Params& p) {
   return (double)rounds * share * f.bm * f.bn * (p.taps * p.d.cp) / f.rate;  // dummy tiles cost MFMA time too
 }
 
-int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   using namespace rb;
-  if (k >= NR) return direct_launch(k - NR, x, w, p, s);
+  if (k >= NR) return direct_launch(k - NR, x, w, p, s, occ);
   switch (k) {
-    case 0: return launch_ek<R0>(x, w, p, s);
-    case 1: return launch_ek<R1>(x, w, p, s);
-    case 2: return launch_ek<R3>(x, w, p, s);
-    default: return launch_ek<R4>(x, w, p, s);
+    case 0: return launch_ek<R0>(x, w, p, s, occ);
+    case 1: return launch_ek<R1>(x, w, p, s, occ);
+    case 2: return launch_ek<R3>(x, w, p, s, occ);
+    case 3: return launch_ek<R4>(x, w, p, s, occ);
+    default: return launch_ek<R5>(x, w, p, s, occ);
   }
 }
 

@@ -16,8 +16,8 @@ import torch  # noqa: F401  (binds the process HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
-ABI_VERSION = 6
-CONV_TILES = 33  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
+ABI_VERSION = 7
+CONV_TILES = 34  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -79,6 +79,7 @@ SIGNATURES = {
     "qnn_conv_border_table": [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_float, c_ptr, c_ptr],
     "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
     "qnn_conv_plan": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
+    "qnn_conv_occupancy": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
     "qnn_maxpool_bn": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,

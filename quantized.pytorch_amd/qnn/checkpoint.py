@@ -98,8 +98,10 @@ def load_maybe_calibrate(model, checkpoint, save_dir, model_name, depth, calib_b
                                    "pass calib_batches to calibrate") from e
             model.load_state_dict(sd, strict=False)
             model = _to_device(model, device)
-            set_measure_mode(model, True)
+            # the reference calibrates a freshly built (train-mode) model; set_measure_mode
+            # then puts BatchNorm layers into eval (main.py:182, quantize.py:547-552)
             model.train()
+            set_measure_mode(model, True)
             with torch.no_grad():
                 for x in calib_batches:
                     model(x.to(next(model.parameters()).device))

@@ -13,10 +13,13 @@ the outputs to device 0.  Here:
     issued asynchronously (`submit`): the logits are copied into one of two send
     slots and the gather overlaps the next step's forward;
   * calibration (main.py:154-205, measure mode) runs on every rank's own batches
-    and `allreduce_calibration` merges the running ranges with ONE bucketed
-    all-reduce (the reference's DataParallel keeps replica 0's statistics only,
-    main.py:345; averaging equal-count running averages is the statistic of all
-    ranks' batches).
+    and `allreduce_calibration` merges the running statistics with ONE bucketed
+    all-reduce, weighted by each rank's samples per batch (the reference's
+    DataParallel keeps replica 0's statistics only, main.py:345).  The merged
+    running_min / running_max / running_mean are exactly the statistics of all
+    ranks' samples (means of per-sample or per-element values); QuantMeasure's std
+    and RangeBN's inverse-range scale are nonlinear in the batch, so their merge is
+    the sample-weighted mean of the per-rank values, an approximation.
 The shard/gather logic is backend-agnostic and is tested with `gloo` on CPU.
 """
 import os
@@ -55,15 +58,19 @@ def shard_bounds(global_batch, world, rank):
     return start, start + base + (1 if rank < rem else 0)
 
 
-def allreduce_calibration(model, group=None):
-    """Average every calibrated statistic of `model` over the ranks of `group`: the
+def allreduce_calibration(model, group=None, samples=1):
+    """Merge every calibrated statistic of `model` over the ranks of `group`: the
     running_min / running_max / running_mean / running_var of each QuantMeasure and the
-    running_mean / running_var of each RangeBN, flattened into one fp32 bucket and
-    all-reduced once (RCCL on GPU tensors, gloo on CPU).  Call after every rank ran the
-    same number of measure-mode batches.  No-op for world size 1."""
+    running_mean / running_var of each RangeBN, weighted by `samples` (this rank's samples
+    per calibration batch: its shard size), flattened into one fp32 bucket and all-reduced
+    once (RCCL on GPU tensors, gloo on CPU).  Call after every rank ran the same number
+    of measure-mode batches.  Exact for the extrema means and the means; the std and the
+    RangeBN scale merge as weighted means (module docstring).  No-op for world size 1."""
     from .quantize import QuantMeasure, RangeBN
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
+    if samples <= 0:
+        raise ValueError("allreduce_calibration: samples must be > 0")
     bufs = []
     for m in model.modules():
         if isinstance(m, QuantMeasure):
@@ -72,9 +79,10 @@ def allreduce_calibration(model, group=None):
             bufs += [m.running_mean, m.running_var]
     if not bufs:
         return
-    flat = torch.cat([b.detach().reshape(-1).to(torch.float32) for b in bufs])
+    flat = torch.cat([b.detach().reshape(-1).to(torch.float64) for b in bufs] +
+                     [torch.ones(1, dtype=torch.float64, device=bufs[0].device)]) * float(samples)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-    flat /= dist.get_world_size(group)
+    flat = flat[:-1] / flat[-1]
     off = 0
     with torch.no_grad():
         for b in bufs:
@@ -132,8 +140,6 @@ class ShardedInference:
 
     def submit_output(self, y_local):
         """Start gathering this rank's output `y_local`; returns a _Pending."""
-        if self.world == 1:
-            return _Pending(None, lambda: y_local)
         n_local = y_local.shape[0]
         s, e = self.bounds[self.rank]
         assert n_local == e - s, f"rank {self.rank}: expected a shard of {e - s}, got {n_local}"
@@ -151,6 +157,9 @@ class ShardedInference:
         if prev is not None:
             prev.result()  # the gather that used this slot two submits ago has finished
         send[:n_local].copy_(y_local)  # ordered before the collective on the current stream
+        if self.world == 1:  # no collective: the slot holds the copy until its handle is read
+            slots[k][2] = pend = _Pending(None, lambda: send[:n_local].clone())
+            return pend
         work = dist.gather(send, recv, dst=self.root, group=self.group, async_op=True)
         if self.rank == self.root:
             fn = lambda: torch.cat([b[: e_ - s_] for b, (s_, e_) in zip(recv, self.bounds)])

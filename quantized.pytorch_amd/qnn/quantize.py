@@ -730,6 +730,8 @@ def _cpu_unsupported(what):
 
 
 # ============================================================ tree helpers (:508-610)
+# (the training-only helpers set_bn_is_train / distill_set_train, quantize.py:523-545,
+# :595-599, belong to the distillation trainer and are out of scope: SURVEY.md §2 row 10)
 def is_bn(m):
     return isinstance(m, nn.BatchNorm2d) or isinstance(m, nn.BatchNorm1d)
 
@@ -742,25 +744,6 @@ def recursive_apply(model, func, *args):
     for m in model.children():
         func(m, *args)
         recursive_apply(m, func, *args)
-
-
-def set_bn_is_train(model, train, logger=None, reload_running_estimators=False, reset_running_estimators=False,
-                    freeze_affine=False):
-    def func(m, *args):
-        if is_bn(m):
-            if reload_running_estimators or reset_running_estimators:
-                if (reload_running_estimators and not hasattr(m, "locked_running_mean")) or reset_running_estimators:
-                    m.locked_running_mean = m.running_mean.data.clone()
-                    m.locked_running_var = m.running_var.data.clone()
-                else:
-                    m.running_mean.data = m.locked_running_mean.clone()
-                    m.running_var.data = m.locked_running_var.clone()
-            if freeze_affine:
-                for p in m.parameters():
-                    p.requires_grad = False
-            m.train(train)
-
-    recursive_apply(model, func)
 
 
 def set_measure_mode(model, measure, momentum=None, logger=None):
@@ -802,13 +785,6 @@ def freeze_quant_params(model, freeze=True, include_param_dyn_range=True, moment
             m.freeze_param_dyn_rang = freeze
 
     recursive_apply(model, func)
-
-
-def distill_set_train(model, train):
-    model.train(train)
-    if train:
-        freeze_quant_params(model)
-        set_bn_is_train(model, False)
 
 
 def set_global_quantization_method(model, method="aciq", logger=None):

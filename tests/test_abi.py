@@ -50,7 +50,7 @@ def test_bindings_cover_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.qnn_abi_version() == 6
+    assert lib.qnn_abi_version() == 7
 
 
 def test_argument_validation_without_device(lib):

@@ -184,3 +184,58 @@ def test_allreduce_calibration_world2():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert sorted(q.get(timeout=10) for _ in range(2)) == [(0, True), (1, True)]
+
+
+def test_async_gather_world1_keeps_every_step():
+    """World size 1 (no process group): submit() still copies the engine's static logits
+    into a send slot, so handles read after later forwards return their own step's logits."""
+    w = torch.randn(16, 5, generator=torch.Generator().manual_seed(3))
+    xs = [torch.randn(6, 16, generator=torch.Generator().manual_seed(200 + k)) for k in range(5)]
+    runner = ShardedInference(_StaticEngine(6, w), 6)
+    assert runner.world == 1
+    handles = [runner.submit(x) for x in xs]
+    outs = [h.result() for h in handles]
+    assert all(torch.allclose(o, x @ w, rtol=0, atol=1e-5) for o, x in zip(outs, xs))
+    assert all(o.data_ptr() != runner.model.logits.data_ptr() for o in outs)
+
+
+def _calib_ragged_worker(rank, world, port, sizes, q):
+    from oracle import qnn_oracle as O
+    from qnn import synthetic
+    from qnn.dist import allreduce_calibration
+    from qnn.quantize import QuantMeasure
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    qmod = QuantMeasure(8)
+    batches = [synthetic.input_batch((sum(sizes), 4, 6, 6), 900 + j) for j in range(2)]
+    s = sum(sizes[:rank])
+    st = O.measure_state()
+    for b in batches:  # this rank's shard of each global calibration batch
+        O.calibrate_measure(st, b[s:s + sizes[rank]])
+    with torch.no_grad():
+        for k, v in st.items():
+            getattr(qmod, k).copy_(v)
+    allreduce_calibration(qmod, samples=sizes[rank])
+    one = O.measure_state()  # one process over the whole global batches
+    for b in batches:
+        O.calibrate_measure(one, b)
+    ok = all(torch.allclose(getattr(qmod, k), one[k], rtol=2e-6, atol=0)
+             for k in ("running_min", "running_max", "running_mean"))
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_calibration_ragged_shards_weighted():
+    """Ragged shards (3 and 2 samples per batch): the sample-weighted merge of the extrema
+    means and the mean equals a one-process calibration over the global batches."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calib_ragged_worker, args=(r, 2, port, (3, 2), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert sorted(q.get(timeout=10) for _ in range(2)) == [(0, True), (1, True)]

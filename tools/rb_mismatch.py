@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Where do two tile configurations disagree, in the resident-band kernel's own coordinates?
+
+Drop-in QConv2d forward (mode 0, NCHW fp32) with config A vs config B, then every mismatch
+mapped to (block, wave, lane, accumulator) of the resident-band layout (qconv_rb.hip):
+block = band * nby + channel tile (before the XCD remap), wave (wm, wn), column tile j,
+lane, register r; plus the error in accumulator units (dy / sxsw[c]).
+
+    python tools/rb_mismatch.py --cfg 27 --shape 256 256 3 1 1 256 14 --bm 128 --bn 224 --wgm 4 --wgn 2 --tm 2 --tn 7
+"""
+import argparse
+import collections
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "quantized.pytorch_amd"))
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+from qnn import _lib, synthetic  # noqa: E402
+from qnn.quantize import QConv2d  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", type=int, required=True)
+    ap.add_argument("--ref", type=int, default=5)
+    ap.add_argument("--shape", type=int, nargs=7, default=[256, 256, 3, 1, 1, 256, 14])
+    ap.add_argument("--bm", type=int, default=128)
+    ap.add_argument("--bn", type=int, default=224)
+    ap.add_argument("--wgm", type=int, default=4)
+    ap.add_argument("--wgn", type=int, default=2)
+    ap.add_argument("--tm", type=int, default=2)
+    ap.add_argument("--tn", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--sentinel", action="store_true",
+                    help="launch through the ABI into an output pre-filled with -7777: which mismatches are never-stored")
+    a = ap.parse_args()
+    cin, cout, k, st, pd, N, H = a.shape
+    dev = torch.device("cuda:0")
+    _lib.load()
+    print("library:", _lib.LIB_PATH)
+    m = QConv2d(cin, cout, k, stride=st, padding=pd, bias=False, num_bits_grad=8, biprecision=True)
+    wrap = nn.Sequential(m)
+    synthetic.init_params(wrap, 41)
+    m.quantize_input.running_min.fill_(0.0)
+    m.quantize_input.running_max.fill_(2.75)
+    wrap = wrap.to(dev).eval()
+    x = (synthetic.input_batch((N, cin, H, H), 42, relu=True) * 1.1).to(dev)
+    m.qnn_tile = a.ref + 1
+    with torch.no_grad():
+        ref = wrap(x).clone()
+    d, e = m._last_conv
+    pk = m._qpack
+    s32 = float(torch.tensor(float(2.75 / 255), dtype=torch.float32))
+    sw = (pk.s_w.double() * s32).float().cpu()
+    Ho = Wo = (H + 2 * pd - k) // st + 1
+    if a.sentinel:
+        import ctypes
+        m.qnn_keep_input = True
+    for rep in range(a.reps):
+        m.qnn_tile = a.cfg + 1
+        with torch.no_grad():
+            y = wrap(x).clone()
+        torch.cuda.synchronize()
+        if a.sentinel:
+            d, e = m._last_conv
+            ys = torch.full_like(y, -7777.0)
+            e.out_f32 = ys.data_ptr()
+            _lib.call("qnn_qconv2d_fwd", _lib.ptr(m._last_xq), _lib.ptr(m._qpack.wq), ctypes.byref(d),
+                      ctypes.byref(e), _lib.stream_of(ys))
+            torch.cuda.synchronize()
+            bad = ys != ref
+            never = int((ys == -7777.0).sum())
+            print(f"  sentinel launch: {int(bad.sum())} differ, {never} never stored")
+            if int(bad.sum()) and never < int(bad.sum()):
+                i = bad.nonzero()[:4].tolist()
+                print("   wrong values at", i, [float(ys[tuple(t)]) for t in i], "ref", [float(ref[tuple(t)]) for t in i])
+            y = ys
+        diff = (y != ref)
+        nbad = int(diff.sum())
+        print(f"rep {rep}: cfg {a.cfg} vs {a.ref}: {nbad} of {diff.numel()} differ")
+        if not nbad:
+            continue
+        idx = diff.nonzero().cpu()
+        dy = (y - ref)[diff].cpu()
+        n, c, h, w = idx.unbind(1)
+        acc_err = (dy / sw[c]).round().long()
+        nby = -(-cout // a.bm)
+        img = Ho * Wo
+        per_band_imgs = max(1, a.bn // img) if img <= a.bn else None
+        blocks = collections.Counter()
+        waves = collections.Counter()
+        regs = collections.Counter()
+        errs = collections.Counter()
+        chans = collections.Counter()
+        pix = collections.Counter()
+        for i in range(min(len(idx), 200000)):
+            ni, ci, hi, wi = (int(v) for v in idx[i])
+            if per_band_imgs:
+                band = ni // per_band_imgs
+                q = (ni % per_band_imgs) * img + hi * Wo + wi
+            else:
+                band, q = -1, hi * Wo + wi
+            cl = ci % a.bm
+            blk = band * nby + ci // a.bm
+            wm = cl // (16 * a.tm)
+            it = (cl % (16 * a.tm)) // 16
+            g = (cl % 16) // 4
+            r = cl % 4
+            wn = q // (16 * a.tn)
+            j = (q % (16 * a.tn)) // 16
+            lane = (q % 16) + 16 * g
+            blocks[blk] += 1
+            waves[(wm, wn)] += 1
+            regs[(it, j, r)] += 1
+            errs[int(acc_err[i])] += 1
+            chans[ci] += 1
+            pix[(hi, wi)] += 1
+        print(f"  blocks with errors: {len(blocks)}; top {blocks.most_common(8)}")
+        print(f"  waves (wm, wn): {sorted(waves.items())}")
+        print(f"  acc regs (i, j, r) top: {regs.most_common(12)}")
+        print(f"  acc-unit errors top: {errs.most_common(12)}")
+        print(f"  channels: {len(chans)} distinct, top {chans.most_common(8)}")
+        print(f"  pixels (h, w): {len(pix)} distinct, top {pix.most_common(8)}")
+        print(f"  images: {len(set(int(v) for v in n))} distinct; first mismatches {idx[:6].tolist()}")
+
+
+if __name__ == "__main__":
+    main()
