@@ -324,6 +324,19 @@ int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stri
                    const int8_t* lut0, const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
                    qnn_stream_t stream);
 
+/* The ResNet stem (resnet_quantized.py:171-174, :140-143) in one launch: the contraction of
+ * qnn_qconv2d_fwd (a short reduction, kpad <= 256, 64 output channels: the space-to-depth 7x7/2
+ * stem) with its RangeBN's input codes (mode 1, bn_* of epi, as out_bncode would receive them),
+ * then nn.MaxPool2d(3, 2, 1) of ReLU o RangeBN on those codes and the outputs of
+ * qnn_maxpool_bn: out_code (pooled codes, byte C-tile; nullable) and codes lut{0,1}[c][q*] into
+ * consumer buffers code{0,1} (nullable).  Bitwise qnn_qconv2d_fwd (out_bncode) followed by
+ * qnn_maxpool_bn, without the full-resolution codes ever reaching memory.  pool_ho/pool_wo:
+ * the pooled size ((ho - 1) / 2 + 1). */
+int qnn_qconv2d_maxpool_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
+                            int pool_ho, int pool_wo, uint8_t* out_code, const int8_t* lut0,
+                            const qnn_code_out* code0, const int8_t* lut1, const qnn_code_out* code1,
+                            qnn_stream_t stream);
+
 /* Depthwise QConv2d (groups == c, mobilenet_quantized.py:38-40) fused with its RangeBN and
  * ReLU (:41-42) on padded NHWC8 codes x [n][hp][wp][cp] whose image interior is
  * [pad, pad+h) x [pad, pad+w); taps outside it are skipped (zero padding of x_hat):

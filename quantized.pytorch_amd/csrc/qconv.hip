@@ -1597,6 +1597,38 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   return QNN_OK;
 }
 
+extern "C" int qnn_qconv2d_maxpool_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc,
+                                      const qnn_epilogue* epi, int pool_ho, int pool_wo, uint8_t* out_code,
+                                      const int8_t* lut0, const qnn_code_out* code0, const int8_t* lut1,
+                                      const qnn_code_out* code1, qnn_stream_t stream) {
+  QNN_REQUIRE(desc && epi, "null descriptor");
+  Params p;
+  const int rc0 = conv_params(*desc, *epi, p);
+  if (rc0 != QNN_OK) return rc0;
+  const qnn_epilogue& e = *epi;
+  QNN_REQUIRE(e.mode == 1 && e.bn_mean && e.bn_sq && e.bn_wq && e.bn_bq && e.bn_scale > 0.f,
+              "stem max-pool: mode 1 with the stem's RangeBN");
+  const bool has0 = code0 && code0->ptr, has1 = code1 && code1->ptr;
+  QNN_REQUIRE(!has0 || (lut0 && (((uintptr_t)lut0) & 15) == 0), "code0 needs a 16-B aligned lut0");
+  QNN_REQUIRE(!has1 || (lut1 && (((uintptr_t)lut1) & 15) == 0), "code1 needs a 16-B aligned lut1");
+  QNN_REQUIRE(out_code || has0 || has1, "no output");
+  QNN_REQUIRE(!out_code || (((uintptr_t)out_code) & 15) == 0, "out_code must be 16-byte aligned");
+  auto code16 = [&](const qnn_code_out* o) {
+    return !o || !o->ptr || (o->cp >= desc->cout && o->cp % 16 == 0 && o->scale > 0.f && o->pad >= 0 &&
+                             (((uintptr_t)o->ptr) & 15) == 0);
+  };
+  QNN_REQUIRE(code16(code0) && code16(code1), "bad code output (cp % 16, 16-B aligned)");
+  if (desc->n == 0) return QNN_OK;
+  QNN_REQUIRE(x && wq && e.sxsw && e.sxbw && e.table && e.hcls && e.wcls, "null pointer");
+  QNN_REQUIRE((((uintptr_t)x) & 15) == 0 && (((uintptr_t)wq) & 15) == 0, "x/wq must be 16-byte aligned");
+  qnn_code_out none{};
+  const int rc = stem_pool_launch(x, wq, p, pool_ho, pool_wo, out_code, has0 ? lut0 : nullptr, has0 ? *code0 : none,
+                                  has1 ? lut1 : nullptr, has1 ? *code1 : none, (hipStream_t)stream);
+  if (rc != QNN_OK) return rc;
+  QNN_LAUNCH_CHECK("qnn_qconv2d_maxpool_fwd");
+  return QNN_OK;
+}
+
 extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* blocks_per_cu,
                                   int* lds_bytes, int* grid) {
   QNN_REQUIRE(desc && epi, "null descriptor");

@@ -1,0 +1,270 @@
+// ResNet stem fused with its max-pool: the space-to-depth stem conv (7x7/2 as 4x4 taps x 16
+// channels, resnet_quantized.py:171-174), RangeBN's input quantization of its output
+// (quantize.py:461-462) and nn.MaxPool2d(3, 2, 1) of relu(RangeBN(.)) (resnet_quantized.py:140-143)
+// in one kernel.  The unfused path writes the stem's full-resolution RangeBN codes to HBM and
+// reads them back in qnn_maxpool_bn (103 MB each way at ResNet-18 b128); here they live in LDS.
+//
+// A block owns PR pooled rows of one image (all pooled columns, all 64 channels):
+//  1. the stem rows its windows read (2*PR + 1, fewer at the image edge) are computed as a
+//     direct-fragment conv (qconv_direct.hip: each 16x16x64 B fragment lane is one 16-byte load
+//     of one tap of one input pixel, sum_valid(q') by an all-ones MFMA against the K mask),
+//     with the exact decomposition and EK_BNCODE arithmetic of every other conv kernel
+//     (epi16.h), so the codes are bitwise the unfused kernel's; they go to LDS as
+//     [row][col][64] bytes;
+//  2. every pooled (pixel, 16 channels) reduces its window in LDS with qnn_maxpool_bn's
+//     algorithm (graph.hip): relu o RangeBN is monotone per channel, so the direction is folded
+//     into the codes with an XOR and the window reduction is a bytewise max; outputs as
+//     qnn_maxpool_bn: the pooled codes (byte C-tile, a residual chain start) and the consumer
+//     codes through the per-channel tables (qnn_bn_code_lut).
+// One stem row per block boundary is computed twice (the window overlap), 1/(2*PR) extra.
+#include "qconv_common.h"
+#include "epi16.h"
+
+namespace qnn {
+namespace sp {
+
+constexpr int C = 64;    // stem channels (one 64-channel block, 4 MFMA row tiles)
+constexpr int TM = 4;
+constexpr int NT = 256;  // 4 waves
+constexpr int PR = 2;    // pooled rows per block
+
+struct Cfg {  // what stage_epi expects
+  static constexpr int BM = 64, W = 4;
+};
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t max_u8x4(uint32_t a, uint32_t b) {
+  u16x2 alo = __builtin_bit_cast(u16x2, a & 0x00ff00ffu), ahi = __builtin_bit_cast(u16x2, (a >> 8) & 0x00ff00ffu);
+  u16x2 blo = __builtin_bit_cast(u16x2, b & 0x00ff00ffu), bhi = __builtin_bit_cast(u16x2, (b >> 8) & 0x00ff00ffu);
+  u16x2 lo = __builtin_elementwise_max(alo, blo), hi = __builtin_elementwise_max(ahi, bhi);
+  return __builtin_bit_cast(uint32_t, lo) | (__builtin_bit_cast(uint32_t, hi) << 8);
+}
+
+struct Pool {
+  int ho, wo;            // pooled output
+  int nrg;               // row groups per image (ceil(ho / PR))
+  uint8_t* out_code;     // nullable: pooled RangeBN input codes, byte C-tile
+  const int8_t* lut0;    // nullable with code0
+  qnn_code_out c0;
+  const int8_t* lut1;
+  qnn_code_out c1;
+  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc;  // LDS offsets
+};
+
+template <int KS, bool MASKED>
+__global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+                                                       const Params p, const Pool pl) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  const qnn_conv_desc& d = p.d;
+  const qnn_epilogue& e = p.e;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int img = blockIdx.x / pl.nrg, pr0 = (blockIdx.x - img * pl.nrg) * PR;
+  const int npr = min(PR, pl.ho - pr0);
+  // stem rows the windows of pooled rows [pr0, pr0 + npr) read (MaxPool2d(3, 2, 1))
+  const int sr_lo = max(2 * pr0 - 1, 0), sr_hi = min(2 * (pr0 + npr - 1) + 1, d.ho - 1);
+  const int npx = (sr_hi - sr_lo + 1) * d.wo, ntile = (npx + 15) >> 4;
+
+  // ---- staged once: epilogue vectors + border table (stage_epi), code tables, border classes
+  stage_epi<Cfg, EK_BNCODE>(p, x, smem, 0, wave, lane);
+  auto stage_lut = [&](const int8_t* lut, int off) {
+    for (int jl = wave; jl < C / 4; jl += 4)
+      __builtin_amdgcn_global_load_lds((const void*)(lut + jl * 1024 + 16 * lane), (lds_ptr_t)(smem + off + 1024 * jl),
+                                       16, 0, 0);
+  };
+  if (pl.lut0) stage_lut(pl.lut0, pl.lds_lut0);
+  if (pl.lut1) stage_lut(pl.lut1, pl.lds_lut1);
+  int* s_hc = reinterpret_cast<int*>(smem + pl.lds_hc);
+  for (int i = tid; i < d.ho + d.wo; i += NT) s_hc[i] = i < d.ho ? e.hcls[i] * e.nwc : e.wcls[i - d.ho];
+
+  // ---- the K chunks of this lane (qconv_direct.hip): tap u / cpg, 16 channels each
+  const int cpg = d.cp >> 4, kreal = p.taps * cpg;
+  int doff[KS];
+  v4i fa[KS][TM], ones[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int u = 4 * s + g;
+    const int tap = u / cpg, tr = tap / d.kw, tc = tap - tr * d.kw;
+    doff[s] = u < kreal ? (tr * d.wp + tc) * d.cp + 16 * (u - tap * cpg) : -1;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      fa[s][i] = *reinterpret_cast<const v4i*>(w + (int64_t)(16 * i + (lane & 15)) * d.kpad + 64 * s + 16 * g);
+    if constexpr (MASKED) ones[s] = *reinterpret_cast<const v4i*>(d.kmask + 64 * s + 16 * g);
+    else ones[s] = (v4i){0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  }
+  const int lgcp = 4 + p.lgcpt;
+  auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
+    int q = t * 16 + (lane & 15);
+    q = q < npx ? q : npx - 1;  // past the rows: the last pixel again (its store is skipped)
+    lr = q / d.wo;
+    col = q - lr * d.wo;
+    const int base = (int)(__umul24(__umul24((unsigned)img, (unsigned)d.hp) + (unsigned)((sr_lo + lr) * d.sh),
+                                    (unsigned)d.wp) + (unsigned)(col * d.sw)) << lgcp;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) fb[s] = *reinterpret_cast<const v4i*>(x + (doff[s] >= 0 ? base + doff[s] : d.zero_off));
+  };
+
+  wait_vmcnt<0>();  // staged data, tables and weights
+  __syncthreads();
+
+  const float* s_f = reinterpret_cast<const float*>(smem);
+  const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+  float4 sw[TM], bw[TM], bi[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int cl = 16 * i + 4 * g;
+    sw[i] = *reinterpret_cast<const float4*>(s_f + cl);
+    bw[i] = *reinterpret_cast<const float4*>(s_f + C + cl);
+    bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * C + cl);
+  }
+  uint8_t* s_codes = reinterpret_cast<uint8_t*>(smem + pl.lds_codes);
+
+  // ---- 1. stem tiles: wave w takes tiles w, w + 4, ...; the next tile's fragments load
+  //         under this one's epilogue
+  v4i fnx[KS];
+  int nlr, ncol;
+  if (wave < ntile) load_b(wave, fnx, nlr, ncol);
+  for (int t = wave; t < ntile; t += 4) {
+    v4i fb[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) fb[s] = fnx[s];
+    const int lr = nlr, col = ncol;
+    if (t + 4 < ntile) load_b(t + 4, fnx, nlr, ncol);
+    v4i acc[TM], sacc = (v4i){0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i] = (v4i){0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      sacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], sacc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], acc[i], 0, 0, 0);
+    }
+    const int pc = s_hc[sr_lo + lr] + s_hc[d.ho + col];
+    const f2 p2 = {(float)sacc[0], (float)sacc[0]};
+    const bool ok = t * 16 + (lane & 15) < npx;
+    uint8_t* dst = s_codes + (lr * d.wo + col) * C + 4 * g;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cl = 16 * i + 4 * g;
+      const float4 tb = *reinterpret_cast<const float4*>(s_f + (7 + pc) * C + cl);
+      const v4i& a = acc[i];
+      const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
+      // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
+      const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
+                    (f2){bi[i].x, bi[i].y};
+      const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
+                    (f2){bi[i].z, bi[i].w};
+      const int kb = pack4(qclamp2(v0, bnp) + MAGIC_U8, qclamp2(v1, bnp) + MAGIC_U8);  // EK_BNCODE
+      if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb;
+    }
+  }
+  // pool direction per channel: 0xff where relu o RangeBN is non-increasing (sq * wq < 0)
+  uint8_t* s_dir = reinterpret_cast<uint8_t*>(smem + pl.lds_dir);
+  if (tid < C) s_dir[tid] = (s_f[4 * C + tid] * s_f[5 * C + tid]) < 0.f ? 0xff : 0;
+  __syncthreads();
+
+  // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest
+  const int ct = (C + 31) >> 5;
+  for (int it = tid; it < npr * pl.wo * 4; it += NT) {
+    const int cg = it & 3, pxi = it >> 2;
+    const int prl = pxi / pl.wo, pc = pxi - prl * pl.wo;
+    const int oy = pr0 + prl, cb = 16 * cg;
+    const uint4 dm = *reinterpret_cast<const uint4*>(s_dir + cb);
+    uint4 best = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int sy = 2 * oy - 1 + r;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int sx = 2 * pc - 1 + s2;
+        // MaxPool2d pads with -inf: an out-of-image tap reads a clamped pixel and is masked
+        // to 0, the identity of the folded-code max
+        const bool okt = sy >= 0 && sy < d.ho && sx >= 0 && sx < d.wo;
+        const int ly = min(max(sy, sr_lo), sr_hi) - sr_lo, lx = min(max(sx, 0), d.wo - 1);
+        const uint4 v = *reinterpret_cast<const uint4*>(s_codes + (ly * d.wo + lx) * C + cb);
+        const uint32_t msk = okt ? 0xffffffffu : 0u;
+        best.x = max_u8x4(best.x, (v.x ^ dm.x) & msk);
+        best.y = max_u8x4(best.y, (v.y ^ dm.y) & msk);
+        best.z = max_u8x4(best.z, (v.z ^ dm.z) & msk);
+        best.w = max_u8x4(best.w, (v.w ^ dm.w) & msk);
+      }
+    }
+    const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
+    const int64_t m = ((int64_t)img * pl.ho + oy) * pl.wo + pc;
+    if (pl.out_code) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int ch = cb + 4 * s4;
+        *reinterpret_cast<uint32_t*>(pl.out_code + btile_off((int)(m >> 5), ch >> 5, ct, (int)(m & 31) + 32 * ((ch >> 2) & 1)) +
+                                     4 * ((ch & 31) >> 3)) = qd[s4];
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const qnn_code_out& co = o ? pl.c1 : pl.c0;
+      if (!co.ptr) continue;
+      const int8_t* sl = smem + (o ? pl.lds_lut1 : pl.lds_lut0);
+      int r4[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        r4[s4] = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ch = cb + 4 * s4 + u;
+          r4[s4] |= ((int)(uint8_t)sl[ch * 256 + ((qd[s4] >> (8 * u)) & 255)]) << (8 * u);
+        }
+      }
+      *reinterpret_cast<int4*>(co.ptr + (((int64_t)img * co.hp + oy + co.pad) * co.wp + pc + co.pad) * co.cp + cb) =
+          make_int4(r4[0], r4[1], r4[2], r4[3]);
+    }
+  }
+}
+
+template <int KS, bool MASKED>
+static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool& pl0, hipStream_t s) {
+  auto kern = stem_pool_kernel<KS, MASKED>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  Pool pl = pl0;
+  int off = (4 * (7 + p.e.nclass) * C + 15) & ~15;  // stage_epi's EK_BNCODE data
+  pl.lds_hc = off;
+  off += (4 * (p.d.ho + p.d.wo) + 15) & ~15;
+  pl.lds_dir = off;
+  off += C;
+  pl.lds_lut0 = off;
+  off += pl.lut0 ? 256 * C : 0;
+  pl.lds_lut1 = off;
+  off += pl.lut1 ? 256 * C : 0;
+  pl.lds_codes = off;
+  off += (2 * PR + 1) * p.d.wo * C;
+  if (off > LDS_MAX) return arg_error("stem max-pool tile needs more than 160 KiB of LDS");
+  const int nblk = p.d.n * pl.nrg;
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(NT), off, s, x, w, p, pl);
+  return QNN_OK;
+}
+
+}  // namespace sp
+
+int stem_pool_launch(const int8_t* x, const int8_t* w, const Params& p, int pool_ho, int pool_wo, uint8_t* out_code,
+                     const int8_t* lut0, const qnn_code_out& c0, const int8_t* lut1, const qnn_code_out& c1,
+                     hipStream_t s) {
+  using namespace sp;
+  const qnn_conv_desc& d = p.d;
+  if (d.cout != C || d.cout_pad < C || d.kpad > 256 || d.kpad % 64 || d.cp % 16 || p.taps * d.cp > d.kpad)
+    return arg_error("stem max-pool: 64 output channels and a short reduction (kpad <= 256) only");
+  if (pool_ho != (d.ho + 2 - 3) / 2 + 1 || pool_wo != (d.wo + 2 - 3) / 2 + 1)
+    return arg_error("stem max-pool: MaxPool2d(3, 2, 1) output size expected");
+  Pool pl{};
+  pl.ho = pool_ho, pl.wo = pool_wo, pl.nrg = (pool_ho + PR - 1) / PR;
+  pl.out_code = out_code, pl.lut0 = lut0, pl.c0 = c0, pl.lut1 = lut1, pl.c1 = c1;
+  const bool m = d.kmask != nullptr;
+  switch ((p.taps * (d.cp >> 4) + 3) >> 2) {
+    case 1: return m ? launch<1, true>(x, w, p, pl, s) : launch<1, false>(x, w, p, pl, s);
+    case 2: return m ? launch<2, true>(x, w, p, pl, s) : launch<2, false>(x, w, p, pl, s);
+    case 3: return m ? launch<3, true>(x, w, p, pl, s) : launch<3, false>(x, w, p, pl, s);
+    default: return m ? launch<4, true>(x, w, p, pl, s) : launch<4, false>(x, w, p, pl, s);
+  }
+}
+
+}  // namespace qnn

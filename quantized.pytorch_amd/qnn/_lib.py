@@ -82,6 +82,8 @@ SIGNATURES = {
     "qnn_conv_occupancy": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr],
+    "qnn_qconv2d_maxpool_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_int, c_int, c_ptr,
+                                c_ptr, _PC, c_ptr, _PC, c_ptr],
     "qnn_maxpool_bn": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,
                        c_int, c_ptr, c_ptr, _PC, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,

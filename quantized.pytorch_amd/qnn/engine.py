@@ -73,10 +73,13 @@ class Engine:
     the model's device).  `engine.input` is a static input buffer; passing it (or
     nothing) avoids the copy.  graph=False runs the launches eagerly (debugging)."""
 
-    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None):
+    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None, fuse_stem_pool=True):
         """tile=k forces tile configuration k on every contraction it is built for (the
         others keep the cost model's choice); tile=None autotunes (or the cost model
-        when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile."""
+        when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile.
+        fuse_stem_pool: the ResNet stem conv and its max-pool as one launch
+        (qnn_qconv2d_maxpool_fwd) where the shapes allow; False keeps two launches."""
+        self.fuse_stem_pool = fuse_stem_pool
         if model.training:
             raise RuntimeError("qnn.Engine: call model.eval() first (the engine is the eval forward)")
         self.model = model
@@ -198,7 +201,7 @@ class Engine:
         self.launch_meta.append({"kernel": name, "ops": int(ops), "bytes": int(nbytes), "shape": shape})
 
     def _conv(self, conv, src, H, W, bn=None, chain=None, relu=False, outs=(), out_f32=None, out_bncode=None,
-              bncode_tiled=False, mode=1, logits=None):
+              bncode_tiled=False, mode=1, logits=None, pool=None):
         """One fused contraction.  src: (buf, CodeOut, geom) of conv's input codes, or a
         ('s2d', buf, geom) tuple for a space-to-depth stem.  chain: the residual added
         after RangeBN (an _Act.res); out_bncode: RangeBN's input codes (byte C-tile when
@@ -266,9 +269,22 @@ class Engine:
         xbuf = src[1] if s2d else src[0]
         self.keep += [pk, sxsw, sxbw, table, g, d, e, xbuf]
         xp, wp_, dp, ep = _lib.ptr(xbuf), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e)
-        self.convs.append((len(self.ops), d, e))
         M = self.N * Ho * Wo
         ops = 2 * M * cout * cin // (conv.groups if isinstance(conv, QConv2d) else 1) * kh * kw
+        if pool is not None:  # conv -> RangeBN codes -> MaxPool2d(3, 2, 1) -> consumers, one launch
+            pho, pwo, pcode, luts, pouts = pool
+            pc = _lib.ptr(pcode)
+            l0 = _lib.ptr(luts[0]) if len(luts) > 0 else None
+            l1 = _lib.ptr(luts[1]) if len(luts) > 1 else None
+            r0 = ctypes.byref(pouts[0]) if len(pouts) > 0 else None
+            r1 = ctypes.byref(pouts[1]) if len(pouts) > 1 else None
+            Mp = self.N * pho * pwo
+            nbytes = geom["nbytes"] + pk.cout_pad * pk.kpad + Mp * cout * (len(pouts) + (1 if pcode is not None else 0))
+            self._add("qnn_qconv2d_maxpool_fwd", lambda st: _lib.call(
+                "qnn_qconv2d_maxpool_fwd", xp, wp_, dp, ep, pho, pwo, pc, l0, r0, l1, r1, st), ops, nbytes,
+                [M, cout, kh * kw * cin])
+            return Ho, Wo
+        self.convs.append((len(self.ops), d, e))
         out_b = M * cout * ((4 if out_f32 is not None or mode == 0 else 0) + len(outs) +
                             (1 if out_bncode is not None else 0))
         if chain is not None:
@@ -337,9 +353,10 @@ class Engine:
         if has_pool:
             mp = model.maxpool
             pk_, ps_, pp_ = mp.kernel_size, mp.stride, mp.padding
-            bncode = torch.empty((N, Ho, Wo, conv1.out_channels), dtype=torch.uint8, device=self.dev)
-            self.keep.append(bncode)
-            self._conv(conv1, src, H, W, bn=bn1, relu=True, out_bncode=bncode)
+            # conv -> RangeBN codes -> max-pool as ONE launch (qnn_qconv2d_maxpool_fwd) for the
+            # space-to-depth 64-channel stem and MaxPool2d(3, 2, 1); else two
+            fused = (self.fuse_stem_pool and isinstance(src[0], str) and conv1.out_channels == 64 and
+                     (pk_, ps_, pp_) == (3, 2, 1) and not mp.ceil_mode and mp.dilation == 1)
             Hp_ = (Ho + 2 * pp_ - pk_) // ps_ + 1
             x_act = _Act(Hp_, Hp_, conv1.out_channels)
             cons, _ = self._block_consumers(blocks[0])
@@ -356,20 +373,26 @@ class Engine:
                 lut = torch.empty((C, 256), dtype=torch.int8, device=self.dev)
                 _lib.call("qnn_bn_code_lut", ctypes.byref(b), C, 1, ctypes.byref(co), _lib.ptr(lut), st)
                 luts.append(lut)
-            self.keep += [bncode] + luts + list(outs)
-            c0 = outs[0] if len(outs) > 0 else None
-            c1 = outs[1] if len(outs) > 1 else None
-            a = (N, Ho, Wo, C, pk_, ps_, pp_, Hp_, Hp_)
-            pc, qp = _lib.ptr(pcode), _lib.ptr(bncode)
-            l0 = _lib.ptr(luts[0]) if len(luts) > 0 else None
-            l1 = _lib.ptr(luts[1]) if len(luts) > 1 else None
-            r0 = None if c0 is None else ctypes.byref(c0)
-            r1 = None if c1 is None else ctypes.byref(c1)
-            br = ctypes.byref(b)
-            self._add("qnn_maxpool_bn", lambda st: _lib.call(
-                "qnn_maxpool_bn", qp, *a, br, 1, None, 1, pc, l0, r0, l1, r1, st), 0,
-                N * Ho * Wo * C + N * Hp_ * Hp_ * C * (len(outs) + (1 if pcode is not None else 0)),
-                [N, Ho, Wo, C])
+            self.keep += luts + list(outs)
+            if fused:
+                self._conv(conv1, src, H, W, bn=bn1, relu=True, pool=(Hp_, Hp_, pcode, luts, outs))
+            else:
+                bncode = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=self.dev)
+                self.keep.append(bncode)
+                self._conv(conv1, src, H, W, bn=bn1, relu=True, out_bncode=bncode)
+                c0 = outs[0] if len(outs) > 0 else None
+                c1 = outs[1] if len(outs) > 1 else None
+                a = (N, Ho, Wo, C, pk_, ps_, pp_, Hp_, Hp_)
+                pc, qp = _lib.ptr(pcode), _lib.ptr(bncode)
+                l0 = _lib.ptr(luts[0]) if len(luts) > 0 else None
+                l1 = _lib.ptr(luts[1]) if len(luts) > 1 else None
+                r0 = None if c0 is None else ctypes.byref(c0)
+                r1 = None if c1 is None else ctypes.byref(c1)
+                br = ctypes.byref(b)
+                self._add("qnn_maxpool_bn", lambda st: _lib.call(
+                    "qnn_maxpool_bn", qp, *a, br, 1, None, 1, pc, l0, r0, l1, r1, st), 0,
+                    N * Ho * Wo * C + N * Hp_ * Hp_ * C * (len(outs) + (1 if pcode is not None else 0)),
+                    [N, Ho, Wo, C])
         else:
             x_act = _Act(Ho, Wo, conv1.out_channels)
             cons, _ = self._block_consumers(blocks[0])
