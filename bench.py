@@ -27,6 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec, 8-bit ResNet-18 224×224 @1/2/4/8 GPU; % int8-MFMA roofline"
+ROUND = 3  # profiles/rNN_traffic_* from an earlier round measured other kernels: never cited as traffic
 PEAK_INT8_TOPS = 5000.0   # dense int8 MFMA, 256 CU x 2.4 GHz (MI355X_MICROARCH.md: 2x bf16 2.5 PF)
 PEAK_HBM_GBS = 8000.0
 
@@ -190,18 +191,33 @@ def model_name(arch, depth):
 
 def pmc_traffic(arch, depth, batch):
     """HBM bytes per forward of the conv launches, from the committed rocprofv3 PMC passes of
-    this workload (tools/traffic.py: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE).
-    None when no summary for this exact workload is committed."""
+    this workload (tools/layer_table.py pmc: FETCH_SIZE x2 per the gfx950 correction +
+    WRITE_SIZE).  None when no summary for this exact workload is committed; a summary from an
+    earlier round than ROUND measured earlier kernels and is reported as stale, never as traffic."""
     import glob
     import re
     paths = glob.glob(os.path.join(HERE, "profiles", f"r*_traffic_{model_name(arch, depth)}_b{batch}.json"))
     if not paths:
         return None
-    latest = max(paths, key=lambda p: int(re.search(r"r(\d+)_traffic", os.path.basename(p)).group(1)))
+    rnd = lambda p: int(re.search(r"r(\d+)_traffic", os.path.basename(p)).group(1))  # noqa: E731
+    latest = max(paths, key=rnd)
+    if rnd(latest) < ROUND:
+        return {"stale": f"profiles/{os.path.basename(latest)} (round {rnd(latest)} kernels; not this round's)"}
     with open(latest) as f:
         d = json.load(f)
     d["source"] = f"profiles/{os.path.basename(latest)}: " + d["source"]
     return d
+
+
+def conv_kernels(engine):
+    """'qconv_rb_kernel x9, qconv_kernel x8, ...': the device functions of one forward's
+    contraction launches (the autotuned tile configurations, qnn_conv_tile_kernel)."""
+    import collections
+    from qnn import _lib
+    c = collections.Counter(_lib.tile_kernel(k) for k, _ in engine.tiles)
+    if "qnn_qconv2d_maxpool_fwd" in engine.launch_names:
+        c["stem_pool_kernel"] += engine.launch_names.count("qnn_qconv2d_maxpool_fwd")
+    return ", ".join(f"{k} x{v}" for k, v in c.most_common())
 
 
 def main():
@@ -254,7 +270,7 @@ def main():
     per_kernel = {}
     for n, ms in d:
         per_kernel[n] = per_kernel.get(n, 0.0) + ms / reps
-    conv_ms_per_fwd = per_kernel.get("qnn_qconv2d_fwd", 0.0)
+    conv_ms_per_fwd = per_kernel.get("qnn_qconv2d_fwd", 0.0) + per_kernel.get("qnn_qconv2d_maxpool_fwd", 0.0)
     launches = engine.num_launches
 
     module_ips = None
@@ -275,6 +291,7 @@ def main():
         achieved = mfma_ops / (conv_ms_per_fwd * 1e-3) / 1e12
         pmc = pmc_traffic(args.model, args.depth, args.batch)
         nconv = sum(1 for n in engine.launch_names if n == "qnn_qconv2d_fwd")
+        nstem = sum(1 for n in engine.launch_names if n == "qnn_qconv2d_maxpool_fwd")
         line = {
             "metric": METRIC,
             "value": round(throughput(args.batch * world, args.steps, elapsed), 2),
@@ -293,12 +310,14 @@ def main():
                                    f"(hipGraph), per-GPU batch {args.batch}",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "model_gop_per_batch": round(total_ops / 1e9, 2)},
-            "roofline": {"bound": "mfma", "kernel": f"qconv_kernel (all {nconv} QConv2d/QLinear launches of one forward)",
+            "roofline": {"bound": "mfma",
+                         "kernel": f"int8 contraction launches of one forward ({nconv} qnn_qconv2d_fwd + "
+                                   f"{nstem} fused stem): {conv_kernels(engine)}",
                          "achieved": round(achieved, 2), "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_INT8_TOPS, 4),
-                         "traffic": None if pmc is None else pmc.get("conv_hbm_bytes_per_forward",
-                                                                      pmc["hbm_bytes_per_forward"]),
-                         "traffic_source": None if pmc is None else pmc["source"],
+                         "traffic": None if pmc is None or "stale" in pmc else
+                         pmc.get("conv_hbm_bytes_per_forward", pmc["hbm_bytes_per_forward"]),
+                         "traffic_source": None if pmc is None else pmc.get("source", "stale: " + pmc.get("stale", "")),
                          "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
                          "model_frac": round(total_ops / (ms_per_step * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4)},
             "engine": {"launches_per_forward": launches, "hipgraph": True,

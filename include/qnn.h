@@ -241,6 +241,13 @@ int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* 
  * not built for the layer / epilogue kind is an argument error. */
 int qnn_conv_tile_count(void);
 
+/* The kernel family of tile configuration `cfg` (0-based, as qnn_conv_plan reports it): the
+ * device function's name -- "qconv_kernel" (LDS-DMA ring), "qconv_pp_kernel" (ping-pong),
+ * "qconv_band_kernel", "qconv16_kernel", "qconv_rb_kernel" (resident band) or
+ * "qconv_direct_kernel" -- as rocprof's kernel trace names its dispatches; NULL when out of
+ * range.  No GPU work. */
+const char* qnn_conv_tile_kernel(int cfg);
+
 /* Depthwise (groups == cin == cout) eval forward: fake-quantize-on-load of x
  * (QuantMeasure range) times the dequantized weights w_hat [c][kh*kw] plus the
  * fake-quantized bias, fp32.  NCHW in, NCHW out. */

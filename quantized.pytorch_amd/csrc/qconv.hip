@@ -1578,6 +1578,15 @@ static int conv_params(const qnn_conv_desc& d, const qnn_epilogue& e, Params& p)
 
 extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
+extern "C" const char* qnn_conv_tile_kernel(int k) {
+  if (k < 0 || k >= ncfg_all()) return nullptr;
+  if (k >= rb_first()) return k - rb_first() < rb_count() - direct_count() ? "qconv_rb_kernel" : "qconv_direct_kernel";
+  if (k >= NCFG) return "qconv16_kernel";
+  if (k >= 12) return "qconv_band_kernel";
+  if (k >= 6 && k <= 9) return "qconv_pp_kernel";
+  return "qconv_kernel";
+}
+
 extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi, int* cfg, int* bm, int* bn,
                              int* nblk) {
   QNN_REQUIRE(desc && epi, "null descriptor");

@@ -17,7 +17,7 @@
 //   swizzle, no padding; a tap shift is one uniform add.  Tiles that straddle an output row
 //   end see at most 2-way conflicts.
 // * A = the weights straight from the packed rows ([cout_pad][kpad], tap-major) into VGPRs,
-//   one global_load_dwordx4 per 16-channel tile per K step, prefetched DA steps ahead.  Each
+//   one global_load_dwordx4 per 16-channel tile per K step, prefetched DA - 1 steps ahead.  Each
 //   wave owns its own output channels, so nothing is shared and nothing synchronises.  K
 //   steps run plane-pair major (g = 2gp, 2gp+1 for each tap), so the two loads of a pair
 //   consume each 128-byte weight line whole, back to back.
@@ -36,6 +36,10 @@
 #endif
 #ifndef QNN_RB_ASM
 #define QNN_RB_ASM 1  // 1: band reads as inline asm with hand-counted lgkmcnt; 0: compiler-scheduled
+#endif
+#ifndef QNN_RB_AGPR
+#define QNN_RB_AGPR 0  // 1: accumulators in AGPRs (an 'a'-constrained asm operand makes the
+                       // compiler select the AGPR form of the MFMAs)
 #endif
 #ifndef QNN_STAMP
 #define QNN_STAMP 0  // diagnostic builds only (make stamp_rb): per-wave s_memtime phase stamps
@@ -75,8 +79,8 @@ __device__ __forceinline__ void lds_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// WGM x WGN waves; a wave owns TM 16-channel tiles x TN 16-pixel tiles; DA K steps of
-// weights in flight per wave; BPC blocks per CU the registers and LDS must allow.
+// WGM x WGN waves; a wave owns TM 16-channel tiles x TN 16-pixel tiles; DA weight register
+// slots per wave (DA - 1 K steps in flight); BPC blocks per CU the registers and LDS must allow.
 template <int WGM_, int WGN_, int TM_, int TN_, int DA_, int BPC_>
 struct Cfg {
   static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, DA = DA_, BPC = BPC_;
@@ -207,6 +211,12 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   };
   auto kbytes = [&](const Cur& c) { return c.t * d.cp + 64 * (H * c.gp + c.h); };
 
+  // DA register slots, DA - 1 K steps of weights in flight: step s computes from slot s % DA and
+  // then refills slot (s - 1) % DA, whose last reader (step s - 1's MFMAs) issued a whole step of
+  // MFMAs earlier.  Refilling the slot the step has just read lets a load's asynchronous return
+  // overwrite an A operand the matrix core has not finished reading when another workgroup's
+  // MFMAs hold the XDL pipe (the two-blocks-per-CU corruption of row 12 of an A fragment,
+  // DESIGN.md §4; tools/asm_mfma_war_check.py finds such loads in the ISA).
   v4i fa[DA][TM];
   Cur cl = {0, 0, 0, 0, 0};  // the next step to load
   auto load_a = [&](v4i (&dst)[TM]) {
@@ -221,7 +231,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     if (H * cl.gp + cl.h < d.cp / 64 - 1 || cl.t < p.taps - 1 || cl.h < H - 1) advance(cl);  // clamp at the last step
   };
 #pragma unroll
-  for (int s = 0; s < DA; ++s) load_a(fa[s]);
+  for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
   // LDS constants and the epilogue's data (their loads wait behind the band and the weights)
   int* s_tap = reinterpret_cast<int*>(smem + g.tap_off);
   int* s_hc = reinterpret_cast<int*>(smem + g.cls_off);  // border classes: hcls[ho] * nwc, wcls[wo]
@@ -237,6 +247,13 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+#if QNN_RB_AGPR
+  {
+    int z = 0;
+    asm volatile("; agpr form" : "+a"(z));
+    if (z == 0x7fffffff) p.e.out_f32[0] = 1.f;
+  }
+#endif
 
   // the band's group 0, the weights and the epilogue data have landed for this wave
   wait_vmcnt<0>();
@@ -283,7 +300,10 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
         }
       }
     });
-    load_a(fa[SL]);
+    // the refill goes after this step's MFMAs (the asm path's last lds_wait already fences all
+    // but the last fragment's): slot (SL + DA - 1) % DA was last read one step earlier
+    __builtin_amdgcn_sched_barrier(0);
+    load_a(fa[(SL + DA - 1) % DA]);
     advance(cc);
   };
 #pragma nounroll
@@ -573,12 +593,20 @@ static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStrea
 //   2   256 x 224               8 (64 x 112)      1          14x14 images, each band fragment feeds 4 MFMAs
 //   3   128 x 256               8 (64 x 64)       1          128-channel tiles, 4 MFMAs per fragment
 //   4   128 x 128               8 (32 x 64)       2          two co-resident blocks (<= 128 VGPRs, <= 80 KiB LDS)
+//   5   64 x 224                4 (32 x 112)      3          64-channel layers: 4 rows of 56, 7 rows of 28
+//   6   64 x 128                4 (32 x 64)       4          64-channel layers: 2 rows of 56, many small blocks
+//   7   64 x 448                8 (32 x 112)      1          64-channel layers: 8 rows of 56
+//   8   256 x 112               8 (32 x 112)      1          half 14x14 images (7 rows): 2 blocks per image
 using R0 = Cfg<8, 1, 2, 13, 3, 1>;
 using R1 = Cfg<4, 2, 2, 7, 3, 1>;
 using R3 = Cfg<4, 2, 4, 7, 3, 1>;
 using R4 = Cfg<2, 4, 4, 4, 3, 1>;
 using R5 = Cfg<4, 2, 2, 4, 3, 2>;
-constexpr int NR = 5;
+using R6 = Cfg<2, 2, 2, 7, 3, 3>;
+using R7 = Cfg<2, 2, 2, 4, 3, 4>;
+using R8 = Cfg<2, 4, 2, 7, 3, 1>;
+using R9 = Cfg<8, 1, 2, 7, 3, 1>;
+constexpr int NR = 9;
 struct Info {
   int bm, bn, w, bpc, acc_tiles;
   float rate;
@@ -589,6 +617,10 @@ static const Info INFO[NR] = {
     {256, 224, 8, 1, 28, 1.45f},
     {128, 256, 8, 1, 16, 1.25f},
     {128, 128, 8, 2, 8, 0.60f},
+    {64, 224, 4, 3, 14, 0.60f},
+    {64, 128, 4, 4, 8, 0.50f},
+    {64, 448, 8, 1, 14, 0.60f},
+    {256, 112, 8, 1, 14, 1.00f},
 };
 
 }  // namespace rb
@@ -647,7 +679,11 @@ int rb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStrea
     case 1: return launch_ek<R1>(x, w, p, s, occ);
     case 2: return launch_ek<R3>(x, w, p, s, occ);
     case 3: return launch_ek<R4>(x, w, p, s, occ);
-    default: return launch_ek<R5>(x, w, p, s, occ);
+    case 4: return launch_ek<R5>(x, w, p, s, occ);
+    case 5: return launch_ek<R6>(x, w, p, s, occ);
+    case 6: return launch_ek<R7>(x, w, p, s, occ);
+    case 7: return launch_ek<R8>(x, w, p, s, occ);
+    default: return launch_ek<R9>(x, w, p, s, occ);
   }
 }
 

@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
 ABI_VERSION = 7
-CONV_TILES = 34  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
+CONV_TILES = 38  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -134,11 +134,27 @@ def load(path=None):
     lib.qnn_measure_stats_work.argtypes = [c_i64]
     lib.qnn_conv_tile_count.restype = c_int
     lib.qnn_conv_tile_count.argtypes = []
+    lib.qnn_conv_tile_kernel.restype = ctypes.c_char_p
+    lib.qnn_conv_tile_kernel.argtypes = [c_int]
     if lib.qnn_conv_tile_count() != CONV_TILES:
         raise QnnLibraryError(f"qnn: library has {lib.qnn_conv_tile_count()} conv tile configurations, "
                               f"bindings expect {CONV_TILES}")
     _lib = lib
     return lib
+
+
+def tile_kernel(cfg):
+    """Kernel family (device function name) of tile configuration `cfg` (0-based, as
+    qnn_conv_plan reports it): qnn_conv_tile_kernel."""
+    n = load().qnn_conv_tile_kernel(int(cfg))
+    if n is None:
+        raise QnnError(f"qnn: no tile configuration {cfg}")
+    return n.decode()
+
+
+def tile_ids(kernel):
+    """The 0-based tile configurations of one kernel family, in id order."""
+    return [k for k in range(CONV_TILES) if tile_kernel(k) == kernel]
 
 
 class LaunchTimer:

@@ -44,7 +44,8 @@ def test_library_exports_every_declared_symbol(lib):
 def test_bindings_cover_every_symbol(lib):
     from qnn import _lib
     for s in declared_symbols():
-        if s in ("qnn_last_error", "qnn_abi_version", "qnn_conv_tile_count", "qnn_measure_stats_work"):
+        if s in ("qnn_last_error", "qnn_abi_version", "qnn_conv_tile_count", "qnn_conv_tile_kernel",
+                 "qnn_measure_stats_work"):
             continue
         assert s in _lib.SIGNATURES, s
 
@@ -77,6 +78,19 @@ def test_argument_validation_without_device(lib):
     assert rc == 1  # 4*c > 16
     # empty batches are a no-op success
     assert lib.qnn_fake_quant_f32(None, None, 0, 0.0, 0.0, 1.0, 255.0, None) == 0
+
+
+def test_tile_kernel_families(lib):
+    """qnn_conv_tile_kernel names every configuration's device function (no GPU work)."""
+    from qnn import _lib
+    fams = [_lib.tile_kernel(k) for k in range(_lib.CONV_TILES)]
+    assert set(fams) == {"qconv_kernel", "qconv_pp_kernel", "qconv_band_kernel", "qconv16_kernel",
+                         "qconv_rb_kernel", "qconv_direct_kernel"}
+    # families are contiguous id ranges, direct-fragment last
+    runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
+    assert len(runs) == len(set(runs)) + 1  # the ring family is split by the ping-pong ids 6-9
+    assert fams[-1] == "qconv_direct_kernel" and len(_lib.tile_ids("qconv_direct_kernel")) == 3
+    assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 
 def test_struct_layout_matches_header():

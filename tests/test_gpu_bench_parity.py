@@ -1,11 +1,14 @@
 """Parity at the benchmark batches and at natural occupancy.
 
-* Resident-band configurations (26-30) at natural occupancy -- as many blocks per CU as
-  registers and LDS allow, no LDS inflation -- on the ResNet-50 b256 shapes (the headline
-  256@14x14 3x3, the K=4608 512@7x7, the 128@28x28 layer-2 3x3) and the 64-channel 56x56
-  band: bitwise against the ring kernel (config 5) and against the oracle at the per-layer
-  bar; configuration 30 must really run two blocks per CU (qnn_conv_occupancy).
-* Direct-fragment configurations (31-33) where every persistent block loops over at least
+* Resident-band configurations (qnn_conv_tile_kernel == "qconv_rb_kernel") at natural
+  occupancy -- as many blocks per CU as registers and LDS allow, no LDS inflation -- on the
+  ResNet-50 b256 shapes (the headline 256@14x14 3x3, the K=4608 512@7x7, the 128@28x28
+  layer-2 3x3) and the 64-channel 56x56 band: bitwise against the ring kernel (config 5) and
+  against the oracle at the per-layer bar; on the headline shape at least one configuration
+  must really run two or more blocks per CU (qnn_conv_occupancy).  This is the test that
+  reproduced the co-residency corruption (a weight load refilling an A operand right after
+  the MFMA that reads it).
+* Direct-fragment configurations where every persistent block loops over at least
   two pixel tiles (the loop and its next-tile prefetch, qconv_direct.hip), against the oracle.
 * The engine at the bench batches of configs C3 (ResNet-50 b256) and C4 (MobileNet b512),
   autotuned, bitwise against the module path (resnet_quantized.py:93-113,
@@ -27,8 +30,15 @@ from qnn.quantize import QConv2d
 pytestmark = pytest.mark.gpu
 
 LAYER_TOL = 1e-5
-RB_FIRST, RB_LAST, DIRECT = 26, 30, (31, 32, 33)
 RING = 5
+
+
+def _rb_ids():
+    return _lib.tile_ids("qconv_rb_kernel")
+
+
+def _direct_ids():
+    return _lib.tile_ids("qconv_direct_kernel")
 
 
 def _occupancy(d, e):
@@ -100,7 +110,7 @@ def test_resident_band_natural_occupancy(gpu, name):
     _close(y_ring[idx], _oracle_rows(wrap.cpu(), x, idx))
     wrap = wrap.to(gpu)
     ran = []
-    for t in range(RB_FIRST, RB_LAST + 1):
+    for t in _rb_ids():
         d.tile = t + 1
         from qnn.engine import Engine
         if not Engine._plan_ok(d, e):
@@ -115,21 +125,21 @@ def test_resident_band_natural_occupancy(gpu, name):
     print(f"{name}: resident-band configurations (id, blocks/CU, grid) = {ran}")
     assert ran, "no resident-band configuration is built for this shape"
     if name.startswith("headline"):
-        two = [r for r in ran if r[0] == RB_LAST]
-        assert two and two[0][1] >= 2 and two[0][2] >= 2 * 256, \
-            f"configuration {RB_LAST} must run two co-resident blocks per CU on a full grid: {two}"
+        two = [r for r in ran if r[1] >= 2 and r[2] >= 2 * 256]
+        assert two, f"no resident-band configuration runs two co-resident blocks per CU on a full grid: {ran}"
 
 
-DIRECT_SHAPES = [  # (name, tile, cin, cout, k, stride, pad, N, H)
-    ("mbn_stem_s2d_3x3_32_b256", 31, 3, 32, 3, 2, 1, 256, 224),
-    ("r_stem_s2d_7x7_64_b128", 32, 3, 64, 7, 2, 3, 128, 224),
-    ("pw_1x1_64_128_56_b256", 33, 64, 128, 1, 1, 0, 256, 56),
+DIRECT_SHAPES = [  # (name, direct-fragment configuration index, cin, cout, k, stride, pad, N, H)
+    ("mbn_stem_s2d_3x3_32_b256", 0, 3, 32, 3, 2, 1, 256, 224),
+    ("r_stem_s2d_7x7_64_b128", 1, 3, 64, 7, 2, 3, 128, 224),
+    ("pw_1x1_64_128_56_b256", 2, 64, 128, 1, 1, 0, 256, 56),
 ]
 
 
 @pytest.mark.parametrize("name", [s[0] for s in DIRECT_SHAPES])
 def test_direct_fragment_persistent_loop(gpu, name):
-    _, tile, cin, cout, k, st, pd, N, H = next(s for s in DIRECT_SHAPES if s[0] == name)
+    _, di, cin, cout, k, st, pd, N, H = next(s for s in DIRECT_SHAPES if s[0] == name)
+    tile = _direct_ids()[di]
     wrap, x = _layer(cin, cout, k, st, pd, N, H, 43)
     wrap = wrap.to(gpu)
     xg = x.to(gpu)
@@ -178,7 +188,7 @@ def test_engine_bench_batch_bitwise_c3_c4(gpu, fixture, batch):
     assert torch.equal(eng.head_input, feat.permute(0, 2, 3, 1)), "engine != module path at the bench batch"
     multi = []
     for (k, _), (_i, dd, ee) in zip(eng.tiles, eng.convs):
-        if k in DIRECT:
+        if k in _direct_ids():
             _, _, _, grid = _occupancy(dd, ee)
             multi.append(_plan(dd, ee)[3] / grid)
     if fixture == "model_mobilenet":

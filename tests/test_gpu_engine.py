@@ -91,7 +91,9 @@ def test_engine_launch_count_resnet18(gpu):
             mod.running_var.fill_(0.5)
     m = m.to(gpu).eval()
     eng = Engine(m, batch=2, graph=False)
-    # s2d quantize + stem conv + maxpool + 20 block convs (incl. 3 downsample) - stem + avgpool + fc
-    assert eng.num_launches == 1 + 1 + 1 + 19 + 1 + 1
+    # s2d quantize + the fused stem conv/max-pool (qnn_qconv2d_maxpool_fwd) + 19 block convs
+    # (incl. 3 downsample) + avgpool + fc
+    assert eng.num_launches == 1 + 1 + 19 + 1 + 1
+    assert eng.launch_names.count("qnn_qconv2d_maxpool_fwd") == 1
     y = eng()
     assert torch.isfinite(y).all()

@@ -66,6 +66,13 @@ def main():
         with torch.no_grad():
             y = wrap(x).clone()
         torch.cuda.synchronize()
+        if rep == 0:
+            import ctypes
+            d, e = m._last_conv
+            cfg, bpc, lds, grid = (ctypes.c_int() for _ in range(4))
+            _lib.call("qnn_conv_occupancy", ctypes.byref(d), ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(bpc),
+                      ctypes.byref(lds), ctypes.byref(grid))
+            print(f"  config {cfg.value}: {bpc.value} blocks/CU, {lds.value} B LDS, grid {grid.value}")
         if a.sentinel:
             d, e = m._last_conv
             ys = torch.full_like(y, -7777.0)
