@@ -137,76 +137,46 @@ __global__ void quantize_nchw_nhwc8_kernel(const float* __restrict__ x, int8_t* 
     *reinterpret_cast<int4*>(q + npix * cp + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
-// Space-to-depth codes (factor 2): z[n][h2][w2][(2u+v)*c + ci], 16 channels.  One block per
-// (S2D_RB s2d rows, image): the 2*S2D_RB*c input rows it needs are read with 16-byte loads
-// (about ten per thread, all in flight together), quantized (quant_code_fast == IEEE
-// division, bit for bit) into an LDS code tile [2*S2D_RB][c][2*wz] whose padding is code' 0,
-// then every thread assembles whole 16-byte s2d pixels from LDS.
-constexpr int S2D_RB = 8;
+// Space-to-depth codes (factor 2): z[n][h2][w2][(2u+v)*c + ci], 16 channels.  One thread per
+// s2d pixel: its 4*c input values (2 rows x 2 columns x c channels, code' 0 outside the image)
+// are loaded together -- for a wave, each of the 4*c loads reads 64 values two floats apart,
+// so every input byte is fetched from HBM once and L1 serves the interleaved half --
+// quantized (quant_code_fast == IEEE division, bit for bit) and stored as one 16-byte pixel.
+// No LDS, no barrier: all 12 loads of every lane are in flight at once.
 __global__ __launch_bounds__(256) void quantize_s2d_kernel(const float* __restrict__ x, int8_t* __restrict__ z, int n,
                                                            int c, int h, int w, int pad, int hz, int wz, float neg_min,
                                                            float scale, float qmax) {
-  extern __shared__ int8_t s_rows[];  // [2*S2D_RB][c][W2] codes'
-  const int W2 = 2 * wz, NR = 2 * S2D_RB, h20 = blockIdx.x * S2D_RB, img = blockIdx.y;
   const float inv = 1.0f / scale;
-  if (n > 0) {
-    for (int i = threadIdx.x; i < NR * c * W2 / 4; i += blockDim.x) reinterpret_cast<int*>(s_rows)[i] = 0;
-    __syncthreads();
-    auto put = [&](int r, int ci, int ix, float v) {
-      const int xx = ix + pad;
-      if (xx < W2) s_rows[(r * c + ci) * W2 + xx] = (int8_t)((int)quant_code_fast(v, neg_min, scale, inv, qmax) - 128);
-    };
-    if ((w & 3) == 0 && (((uintptr_t)x) & 15) == 0) {
-      // batches of B loads issued back to back (rows outside the image read row 0 and are
-      // discarded), then quantized: one HBM round trip per batch, not per load
-      constexpr int B = 12;
-      const int w4 = w >> 2, per_row = c * w4, total = NR * per_row;
-      for (int i0 = 0; i0 < total; i0 += B * (int)blockDim.x) {
-        float4 v[B];
-        int where[B];
+  const int64_t total = (int64_t)n * hz * wz;
+  const int64_t hw = (int64_t)h * w;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int w2 = (int)(i % wz);
+    const int64_t r = i / wz;
+    const int h2 = (int)(r % hz), img = (int)(r / hz);
+    float v[16];
+    bool ok[4];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
-          const int i = i0 + b * blockDim.x + threadIdx.x;
-          const int ii = i < total ? i : total - 1;
-          const int r = ii / per_row, rem = ii - r * per_row, ci = rem / w4, k = rem - ci * w4;
-          const int iy = 2 * h20 - pad + r;
-          const bool ok = i < total && iy >= 0 && iy < h;
-          where[b] = ok ? (r * c + ci) * w4 + k : -1;
-          v[b] = *reinterpret_cast<const float4*>(x + (((size_t)img * c + ci) * h + (ok ? iy : 0)) * w + 4 * k);
-        }
+    for (int uv = 0; uv < 4; ++uv) {
+      const int iy = 2 * h2 + (uv >> 1) - pad, ix = 2 * w2 + (uv & 1) - pad;
+      ok[uv] = iy >= 0 && iy < h && ix >= 0 && ix < w;
+      const float* src = x + (int64_t)img * c * hw + (ok[uv] ? (int64_t)iy * w + ix : 0);
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
-          if (where[b] < 0) continue;
-          const int rc = where[b] / w4, k = where[b] - rc * w4, r = rc / c, ci = rc - r * c;
-          put(r, ci, 4 * k, v[b].x);
-          put(r, ci, 4 * k + 1, v[b].y);
-          put(r, ci, 4 * k + 2, v[b].z);
-          put(r, ci, 4 * k + 3, v[b].w);
-        }
-      }
-    } else {
-      for (int i = threadIdx.x; i < NR * c * w; i += blockDim.x) {
-        const int r = i / (c * w), rem = i - r * c * w, ci = rem / w, ix = rem - ci * w;
-        const int iy = 2 * h20 - pad + r;
-        if (iy >= 0 && iy < h) put(r, ci, ix, x[(((size_t)img * c + ci) * h + iy) * w + ix]);
-      }
+      for (int ci = 0; ci < 4; ++ci) v[uv * 4 + ci] = ci < c ? src[ci * hw] : 0.f;
     }
-    __syncthreads();
-    const int rows = min(S2D_RB, hz - h20);
-    for (int i = threadIdx.x; i < rows * wz; i += blockDim.x) {
-      const int r2 = i / wz, w2 = i - r2 * wz;
-      union {
-        int8_t b[16];
-        int4 v;
-      } out;
-      out.v = make_int4(0, 0, 0, 0);
+    union {
+      int8_t b[16];
+      int4 q;
+    } out;
+    out.q = make_int4(0, 0, 0, 0);
 #pragma unroll
-      for (int uv = 0; uv < 4; ++uv)
-        for (int ci = 0; ci < c; ++ci) out.b[uv * c + ci] = s_rows[((2 * r2 + (uv >> 1)) * c + ci) * W2 + 2 * w2 + (uv & 1)];
-      *reinterpret_cast<int4*>(z + (((size_t)img * hz + h20 + r2) * wz + w2) * 16) = out.v;
-    }
+    for (int uv = 0; uv < 4; ++uv)
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci)
+        if (ci < c && ok[uv])
+          out.b[uv * c + ci] = (int8_t)((int)quant_code_fast(v[uv * 4 + ci], neg_min, scale, inv, qmax) - 128);
+    *reinterpret_cast<int4*>(z + i * 16) = out.q;
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 8)
+  if (blockIdx.x == 0 && threadIdx.x < 8)
     *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
@@ -461,10 +431,9 @@ int qnn_quantize_nchw_to_s2d8(const float* x, int8_t* z, int n, int c, int h, in
   QNN_REQUIRE(scale > 0.f, "scale must be > 0");
   QNN_REQUIRE(z && (n == 0 || x), "null pointer");
   QNN_REQUIRE((((uintptr_t)z) & 15) == 0, "z must be 16-byte aligned");
-  QNN_REQUIRE(n < 65536 && 2 * S2D_RB * c * 2 * wz <= 64 * 1024, "batch >= 65536 or image too wide");
-  const dim3 grid((unsigned)cdiv(hz, S2D_RB), (unsigned)(n > 0 ? n : 1));
-  hipLaunchKernelGGL(quantize_s2d_kernel, grid, dim3(256), 2 * S2D_RB * c * 2 * wz, (hipStream_t)stream, x, z, n, c,
-                     h, w, pad, hz, wz, neg_min, scale, qmax);
+  const int64_t total = (int64_t)n * hz * wz;
+  hipLaunchKernelGGL(quantize_s2d_kernel, dim3(grid_for(total > 0 ? total : 1, 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, z, n, c, h, w, pad, hz, wz, neg_min, scale, qmax);
   QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_s2d8");
   return QNN_OK;
 }

@@ -5,12 +5,14 @@
 // reads them back in qnn_maxpool_bn (103 MB each way at ResNet-18 b128); here they live in LDS.
 //
 // A block owns PR pooled rows of one image (all pooled columns, all 64 channels):
-//  1. the stem rows its windows read (2*PR + 1, fewer at the image edge) are computed as a
-//     direct-fragment conv (qconv_direct.hip: each 16x16x64 B fragment lane is one 16-byte load
-//     of one tap of one input pixel, sum_valid(q') by an all-ones MFMA against the K mask),
-//     with the exact decomposition and EK_BNCODE arithmetic of every other conv kernel
-//     (epi16.h), so the codes are bitwise the unfused kernel's; they go to LDS as
-//     [row][col][64] bytes;
+//  0. the padded space-to-depth input rows those stem rows read -- one contiguous stretch of
+//     the NHWC16 codes -- land in LDS by LDS-DMA (the BAND), with the epilogue data and tables;
+//  1. the stem rows its windows read (2*PR + 1, fewer at the image edge) are computed with
+//     16x16x64 MFMAs whose B fragment lanes are one 16-byte chunk of one tap of one band pixel
+//     (ds_read_b128; every input byte crosses L2 once per block, no global-load latency in the
+//     tile loop), sum_valid(q') by an all-ones MFMA against the K mask, with the exact
+//     decomposition and EK_BNCODE arithmetic of every other conv kernel (epi16.h), so the
+//     codes are bitwise the unfused kernel's; they go to LDS as [row][col][64] bytes;
 //  2. every pooled (pixel, 16 channels) reduces its window in LDS with qnn_maxpool_bn's
 //     algorithm (graph.hip): relu o RangeBN is monotone per channel, so the direction is folded
 //     into the codes with an XOR and the window reduction is a bytewise max; outputs as
@@ -20,16 +22,24 @@
 #include "qconv_common.h"
 #include "epi16.h"
 
+#ifndef QNN_SP_ABLATE
+#define QNN_SP_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no tile epilogue, 3 no pooling, 4 no band DMA
+#endif
+
 namespace qnn {
 namespace sp {
 
 constexpr int C = 64;    // stem channels (one 64-channel block, 4 MFMA row tiles)
 constexpr int TM = 4;
-constexpr int NT = 256;  // 4 waves
-constexpr int PR = 2;    // pooled rows per block
+constexpr int W = 8;     // waves: each takes every W-th 16-pixel stem tile, all 64 channels
+constexpr int NT = 64 * W;
+#ifndef QNN_SP_PR
+#define QNN_SP_PR 4
+#endif
+constexpr int PR = QNN_SP_PR;  // pooled rows per block (4: 9 stem rows, 1/8 of them computed twice)
 
 struct Cfg {  // what stage_epi expects
-  static constexpr int BM = 64, W = 4;
+  static constexpr int BM = 64, W = sp::W;
 };
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -48,7 +58,7 @@ struct Pool {
   qnn_code_out c0;
   const int8_t* lut1;
   qnn_code_out c1;
-  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc;  // LDS offsets
+  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc, lds_band, lds_zero;  // LDS offsets
 };
 
 template <int KS, bool MASKED>
@@ -65,10 +75,22 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   const int sr_lo = max(2 * pr0 - 1, 0), sr_hi = min(2 * (pr0 + npr - 1) + 1, d.ho - 1);
   const int npx = (sr_hi - sr_lo + 1) * d.wo, ntile = (npx + 15) >> 4;
 
+  // ---- the band: padded input rows [R0, R0 + nbr) of this image, one contiguous stretch of
+  // nbr * wp * cp bytes, by 1 KiB LDS-DMA pieces (past its end: the zero page)
+  const int R0 = img * d.hp + sr_lo * d.sh, nbr = (sr_hi - sr_lo) * d.sh + d.kh;
+  const int band_bytes = nbr * d.wp * d.cp;
+  {
+    const int64_t src0 = (int64_t)R0 * d.wp * d.cp;
+    for (int pc = wave; pc * 1024 < band_bytes && QNN_SP_ABLATE != 4; pc += W) {
+      const int o = pc * 1024 + 16 * lane;
+      const int64_t src = o < band_bytes ? src0 + o : (int64_t)d.zero_off;
+      __builtin_amdgcn_global_load_lds((const void*)(x + src), (lds_ptr_t)(smem + pl.lds_band + pc * 1024), 16, 0, 0);
+    }
+  }
   // ---- staged once: epilogue vectors + border table (stage_epi), code tables, border classes
   stage_epi<Cfg, EK_BNCODE>(p, x, smem, 0, wave, lane);
   auto stage_lut = [&](const int8_t* lut, int off) {
-    for (int jl = wave; jl < C / 4; jl += 4)
+    for (int jl = wave; jl < C / 4; jl += W)
       __builtin_amdgcn_global_load_lds((const void*)(lut + jl * 1024 + 16 * lane), (lds_ptr_t)(smem + off + 1024 * jl),
                                        16, 0, 0);
   };
@@ -76,8 +98,10 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   if (pl.lut1) stage_lut(pl.lut1, pl.lds_lut1);
   int* s_hc = reinterpret_cast<int*>(smem + pl.lds_hc);
   for (int i = tid; i < d.ho + d.wo; i += NT) s_hc[i] = i < d.ho ? e.hcls[i] * e.nwc : e.wcls[i - d.ho];
+  if (tid < 4) reinterpret_cast<int*>(smem + pl.lds_zero)[tid] = 0;
 
-  // ---- the K chunks of this lane (qconv_direct.hip): tap u / cpg, 16 channels each
+  // ---- the K chunks of this lane: tap u / cpg, 16 channels each, as band byte offsets from
+  // the tile pixel's tap (0, 0); chunks past the taps read a 16-byte zero slot
   const int cpg = d.cp >> 4, kreal = p.taps * cpg;
   int doff[KS];
   v4i fa[KS][TM], ones[KS];
@@ -92,19 +116,18 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
     if constexpr (MASKED) ones[s] = *reinterpret_cast<const v4i*>(d.kmask + 64 * s + 16 * g);
     else ones[s] = (v4i){0x01010101, 0x01010101, 0x01010101, 0x01010101};
   }
-  const int lgcp = 4 + p.lgcpt;
   auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
     int q = t * 16 + (lane & 15);
     q = q < npx ? q : npx - 1;  // past the rows: the last pixel again (its store is skipped)
     lr = q / d.wo;
     col = q - lr * d.wo;
-    const int base = (int)(__umul24(__umul24((unsigned)img, (unsigned)d.hp) + (unsigned)((sr_lo + lr) * d.sh),
-                                    (unsigned)d.wp) + (unsigned)(col * d.sw)) << lgcp;
+    const int base = pl.lds_band + (lr * d.sh * d.wp + col * d.sw) * d.cp;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) fb[s] = *reinterpret_cast<const v4i*>(x + (doff[s] >= 0 ? base + doff[s] : d.zero_off));
+    for (int s = 0; s < KS; ++s)
+      fb[s] = *reinterpret_cast<const v4i*>(smem + (doff[s] >= 0 ? base + doff[s] : pl.lds_zero));
   };
 
-  wait_vmcnt<0>();  // staged data, tables and weights
+  wait_vmcnt<0>();  // band, staged data, tables and weights
   __syncthreads();
 
   const float* s_f = reinterpret_cast<const float*>(smem);
@@ -119,25 +142,37 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   }
   uint8_t* s_codes = reinterpret_cast<uint8_t*>(smem + pl.lds_codes);
 
-  // ---- 1. stem tiles: wave w takes tiles w, w + 4, ...; the next tile's fragments load
-  //         under this one's epilogue
+  // ---- 1. stem tiles: wave w takes tiles w, w + W, ...; the next tile's fragments are read
+  //         from the band before this one's MFMAs
   v4i fnx[KS];
   int nlr, ncol;
   if (wave < ntile) load_b(wave, fnx, nlr, ncol);
-  for (int t = wave; t < ntile; t += 4) {
+  for (int t = wave; t < ntile; t += W) {
     v4i fb[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) fb[s] = fnx[s];
     const int lr = nlr, col = ncol;
-    if (t + 4 < ntile) load_b(t + 4, fnx, nlr, ncol);
+    if (t + W < ntile) load_b(t + W, fnx, nlr, ncol);
     v4i acc[TM], sacc = (v4i){0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i] = (v4i){0, 0, 0, 0};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+      if (QNN_SP_ABLATE == 1) {
+        asm volatile("" ::"v"(fb[s]));
+        sacc[0] += fb[s][0];
+        continue;
+      }
       sacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], sacc, 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], acc[i], 0, 0, 0);
+    }
+    if (QNN_SP_ABLATE == 2) {
+      int z = sacc[0];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) z ^= acc[i][0] ^ acc[i][1] ^ acc[i][2] ^ acc[i][3];
+      if (t * 16 + (lane & 15) < npx) *reinterpret_cast<int*>(s_codes + (lr * d.wo + col) * C + 4 * g) = z;
+      continue;
     }
     const int pc = s_hc[sr_lo + lr] + s_hc[d.ho + col];
     const f2 p2 = {(float)sacc[0], (float)sacc[0]};
@@ -165,7 +200,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
 
   // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest
   const int ct = (C + 31) >> 5;
-  for (int it = tid; it < npr * pl.wo * 4; it += NT) {
+  for (int it = tid; it < npr * pl.wo * 4 && QNN_SP_ABLATE != 3; it += NT) {
     const int cg = it & 3, pxi = it >> 2;
     const int prl = pxi / pl.wo, pc = pxi - prl * pl.wo;
     const int oy = pr0 + prl, cb = 16 * cg;
@@ -236,6 +271,10 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool&
   off += pl.lut0 ? 256 * C : 0;
   pl.lds_lut1 = off;
   off += pl.lut1 ? 256 * C : 0;
+  pl.lds_zero = off;
+  off += 16;
+  pl.lds_band = off;  // (2 PR + 1) stem rows read (2 PR) * sh + kh padded input rows, 1 KiB DMA pieces
+  off += (int)cdiv((int64_t)(2 * PR * p.d.sh + p.d.kh) * p.d.wp * p.d.cp, 1024) * 1024;
   pl.lds_codes = off;
   off += (2 * PR + 1) * p.d.wo * C;
   if (off > LDS_MAX) return arg_error("stem max-pool tile needs more than 160 KiB of LDS");

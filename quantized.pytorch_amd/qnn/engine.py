@@ -590,12 +590,15 @@ class Engine:
         result, so this only changes speed.  Runs the launch list once first so every
         buffer a conv reads holds real data; re-running a conv is idempotent."""
         st = _lib.stream_of(self.input)
+        self.tune_table = []  # per contraction: {config: ms} of every configuration built for it
         with torch.no_grad():
             self._run_ops()
             self.tiles = []
             for idx, d, _e in self.convs:
                 op = self.ops[idx]
                 best = None
+                times = {}
+                self.tune_table.append(times)
                 for k in range(_lib.CONV_TILES):
                     d.tile = k + 1
                     try:
@@ -609,6 +612,7 @@ class Engine:
                     e1.record()
                     e1.synchronize()
                     ms = e0.elapsed_time(e1) / reps
+                    times[k] = ms
                     if best is None or ms < best[1]:
                         best = (k, ms)
                 if best is None:
