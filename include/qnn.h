@@ -255,6 +255,24 @@ int qnn_dwconv2d_fwd(const float* x, int n, int c, int h, int w, const float* w_
                      int sh, int sw, int ph, int pw, int ho, int wo, float neg_min, float min, float scale,
                      float qmax, const float* bias, float* y, qnn_stream_t stream);
 
+/* ---------------------------------------------------------------- RCCL gather (§8(e)) */
+
+/* The one collective of the data-parallel eval forward: every rank's [B/W, classes] fp32
+ * logits gathered to the root over RCCL (xGMI), replacing nn.DataParallel's gather
+ * (reference main.py:345 scatters the batch and gathers the outputs every forward).  One
+ * process per GPU; the communicator is the library's only global mutable state.
+ *   qnn_comm_unique_id: on one rank, an opaque id (QNN_COMM_ID_BYTES) to share with the others
+ *                       (any out-of-band channel: torch.distributed broadcast, a file, MPI);
+ *   qnn_comm_init:      on every rank, with the same id (ncclCommInitRank; blocks until all join);
+ *   qnn_gather_f32:     recv[r * count .. ] = rank r's send[0 .. count) on the root (recv is
+ *                       ignored elsewhere), enqueued on `stream`;
+ *   qnn_comm_destroy:   collective teardown. */
+#define QNN_COMM_ID_BYTES 128
+int qnn_comm_unique_id(void* id, size_t bytes);
+int qnn_comm_init(int rank, int world, const void* unique_id);
+int qnn_gather_f32(const float* send, float* recv, size_t count, int root, qnn_stream_t stream);
+int qnn_comm_destroy(void);
+
 /* ---------------------------------------------------------------- calibration (§8(f2)) */
 
 /* QuantMeasure's train-branch statistics (models/modules/quantize.py:225-236) of x viewed

@@ -59,7 +59,17 @@ __device__ __forceinline__ float quant_code_fast(float x, float neg_min, float s
 // forms above)
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+#if QNN_SCALAR_FMA
+// two v_fma_f32 (inline asm, so the SLP vectorizer cannot re-form a v_pk_fma_f32)
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) {
+  float x, y;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(x) : "v"(a.x), "v"(b.x), "v"(c.x));
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(y) : "v"(a.y), "v"(b.y), "v"(c.y));
+  return (f2){x, y};
+}
+#else
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+#endif
 
 struct QParams {  // one per-tensor quantizer: x -> code
   float nm, s, inv, lim, qmax;  // -min, scale, RN(1/scale), 2^20*scale, 2^bits-1

@@ -178,3 +178,39 @@ class ShardedInference:
     def __call__(self, x_local):
         with torch.no_grad():
             return self.gather(self.model(x_local))
+
+
+class AbiComm:
+    """The library's own RCCL communicator (include/qnn.h qnn_comm_*): the logits gather
+    through the C ABI, for callers that bind the library without torch.distributed's
+    collectives.  Rank 0 makes the id; it reaches the other ranks over the
+    existing process group (any backend) when world > 1."""
+
+    def __init__(self, rank=0, world=1):
+        import ctypes
+        from . import _lib
+        self.rank, self.world = rank, world
+        uid = (ctypes.c_ubyte * 128)()
+        if rank == 0:
+            _lib.call("qnn_comm_unique_id", ctypes.byref(uid), ctypes.sizeof(uid))
+        if world > 1:
+            t = torch.tensor(list(uid), dtype=torch.uint8)
+            if dist.get_backend() == "nccl":
+                t = t.cuda()
+            dist.broadcast(t, 0)
+            uid = (ctypes.c_ubyte * 128)(*t.cpu().tolist())
+        _lib.call("qnn_comm_init", rank, world, ctypes.byref(uid))
+
+    def gather(self, send, recv=None, root=0):
+        """recv[r * send.numel():...] = rank r's send on the root, on the current stream."""
+        from . import _lib
+        assert send.is_contiguous() and send.dtype == torch.float32
+        if self.rank == root:
+            assert recv is not None and recv.numel() >= send.numel() * self.world and recv.is_contiguous()
+        _lib.call("qnn_gather_f32", _lib.ptr(send), _lib.ptr(recv) if recv is not None else None, send.numel(),
+                  root, _lib.stream_of(send))
+        return recv
+
+    def close(self):
+        from . import _lib
+        _lib.call("qnn_comm_destroy")
