@@ -60,7 +60,7 @@ extern "C" int qnn_comm_destroy(void) {
 extern "C" int qnn_gather_f32(const float* send, float* recv, size_t count, int root, qnn_stream_t stream) {
   QNN_REQUIRE(g_comm, "no communicator (qnn_comm_init)");
   QNN_REQUIRE(root >= 0 && root < g_world, "root out of range");
-  QNN_REQUIRE(send && (g_rank != root || recv), "null buffer");
   if (count == 0) return QNN_OK;
+  QNN_REQUIRE(send && (g_rank != root || recv), "null buffer");
   return nccl_check(ncclGather(send, recv, count, ncclFloat32, root, g_comm, (hipStream_t)stream), "ncclGather");
 }
