@@ -167,14 +167,18 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
   const bool bn_gen = (EK == EK_GEN || (EK == EK_LUT && !use_lut)) && e.bn_mean;
   const int8_t* s_lut = smem + p.epi_off + 4 * (7 + e.nclass) * BM;  // EK_LUT with use_lut: [BM][256]
   constexpr bool CACHE_BN = TM * TN <= 16 && TM <= 2;  // the RangeBN vectors stay in registers beside few accumulators
+  // one pixel tile per lane (TN == 1): nothing to reuse, the channel vectors are read where used
+  constexpr bool CACHE_W = TN > 1;
 
   float4 sw[TM], bw[TM], bi[TM], mn[TM], sq[TM], wq[TM], bq[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int cl = wm * 16 * TM + 16 * i + 4 * g;
-    sw[i] = *reinterpret_cast<const float4*>(s_f + cl);
-    bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cl);
-    bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
+    if (CACHE_W) {
+      sw[i] = *reinterpret_cast<const float4*>(s_f + cl);
+      bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cl);
+      bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
+    }
     if (CACHE_BN && bn_gen) {
       mn[i] = *reinterpret_cast<const float4*>(s_f + 3 * BM + cl);
       sq[i] = *reinterpret_cast<const float4*>(s_f + 4 * BM + cl);
@@ -182,12 +186,18 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
       bq[i] = *reinterpret_cast<const float4*>(s_f + 6 * BM + cl);
     }
   }
+  // EK_LUT, 64 channels per wave: the four 4-byte code words of a pixel (channels 16i + 4g..)
+  // are transposed across the lane groups (two v_permlane32_swap + two v_permlane16_swap), so
+  // lane group g holds the pixel's channels 16g..16g+15 and stores them as one 16-byte word
+  const bool wide = EK == EK_LUT && TM == 4 && use_lut && c0 + wm * 64 + 64 <= d.cout &&
+                    c0 + wm * 64 + 64 <= e.code0_cp;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     Pix P;
     int pc;
     pixel(j, P, pc);
     const int ptab = nparam + pc * BM;
+    unsigned wrd[TM];  // the wide path's code words
     const f2 p2 = {(float)sumq[j], (float)sumq[j]};
     const int mc = P.m;  // a valid pixel (past-the-block slots hold the last one)
     // padded pixel index (its factors < 2^24: full-rate 24-bit multiplies) x cp, 64-bit
@@ -200,6 +210,11 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
       const bool cok = c < d.cout;                   // fused modes: cout % 16 == 0 (4-channel groups all in)
       const int cc = cok ? c : d.cout - 4;
       const float4 tb = *reinterpret_cast<const float4*>(s_f + ptab + cl);
+      if (!CACHE_W) {
+        sw[i] = *reinterpret_cast<const float4*>(s_f + cl);
+        bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cl);
+        bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl);
+      }
       const v4i& a = acc[i][j];
       const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
       f2 v[2];
@@ -226,7 +241,8 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
         int rr = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) rr |= ((int)(uint8_t)s_lut[(cl + u) * 256 + qq[u]]) << (8 * u);
-        if (c < e.code0_cp) *reinterpret_cast<int*>(e.out_code0 + px0 + c) = cok ? rr : 0;
+        if (wide) wrd[i] = (unsigned)rr;
+        else if (c < e.code0_cp) *reinterpret_cast<int*>(e.out_code0 + px0 + c) = cok ? rr : 0;
         continue;
       }
       f2 qb[2];  // RangeBN input: clamped quotient (rounded below)
@@ -331,6 +347,20 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
           *reinterpret_cast<int*>(e.out_code1 + (((int64_t)P.n * e.code1_hp + P.ho + e.code1_pad) * e.code1_wp +
                                                  P.wo + e.code1_pad) * e.code1_cp + c) = k1;
         }
+      }
+    }
+    if constexpr (EK == EK_LUT && TM == 4) {
+      if (wide) {
+        // M[g][i] = wrd[i] of lane group g.  permlane32_swap(r0, r2), (r1, r3) exchange the
+        // upper groups of r0/r1 with the lower groups of r2/r3; permlane16_swap(r0, r1),
+        // (r2, r3) then the odd groups of the first with the even groups of the second:
+        // afterwards register k of group g holds M[k][g], i.e. channels 16g + 4k..
+        const auto s02 = __builtin_amdgcn_permlane32_swap(wrd[0], wrd[2], false, false);
+        const auto s13 = __builtin_amdgcn_permlane32_swap(wrd[1], wrd[3], false, false);
+        const auto t01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+        const auto t23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+        *reinterpret_cast<v4i*>(e.out_code0 + px0 + c0 + wm * 64 + 16 * g) =
+            (v4i){(int)t01[0], (int)t01[1], (int)t23[0], (int)t23[1]};
       }
     }
   }

@@ -23,6 +23,10 @@
 #include "qconv_common.h"
 #include "epi16.h"
 
+#ifndef QNN_ABLATE
+#define QNN_ABLATE 0  // diagnostic builds only: 1 no B loads, 2 no MFMA, 3 no epilogue
+#endif
+
 namespace qnn {
 namespace dk {
 
@@ -30,15 +34,18 @@ namespace dk {
 // 16-pixel tiles.  CB channels per block; BM = max(CB, 64) is the stride of the staged epilogue
 // vectors (stage_epi moves 64 floats per DMA; channels past the block's CB are staged, unused).
 // (WGM, BPC: the members stage_epi / epilogue_rb expect.)
-template <int TM_, int TN_>
+template <int TM_, int TN_, bool K576_ = false, bool PF_ = true>
 struct Cfg {
   static constexpr int WGM = 1, WGN = 4, TM = TM_, TN = TN_, BPC = 1;
+  static constexpr bool K576 = K576_;  // built for exactly nine K steps (3x3 on 64 channels)
+  static constexpr bool PF = PF_;      // prefetch the next tile's fragments under this one's work
   static constexpr int W = WGM * WGN, NT = 64 * W;
   static constexpr int CB = TM * 16, BM = CB < 64 ? 64 : CB, BN = WGN * TN * 16;
   static_assert(CB <= BM, "channel tile wider than the staging stride");
 };
 
-constexpr int KPAD_MAX = 256;
+constexpr int KPAD_MAX = 256;  // configurations 0-2
+constexpr int KS_3X3 = 9;      // configurations 3-4: the 3x3 layers on 64 input channels (K = 576)
 
 // q = m / D, r = m % D for 0 <= m < 2^24 (checked on the host): the float quotient is off by
 // at most one, fixed up exactly -- a few VALU ops where an integer division costs ~40
@@ -50,7 +57,7 @@ __device__ __forceinline__ void fdivmod(int m, int D, float invD, int& q, int& r
 }
 
 template <class C, int EK, bool MASKED, int KS>
-__global__ __launch_bounds__(C::NT) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::PF ? 1 : 2))) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                             const Params p) {
   constexpr int TM = C::TM, TN = C::TN, CB = C::CB, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -110,14 +117,16 @@ __global__ __launch_bounds__(C::NT) void qconv_direct_kernel(const int8_t* __res
       const int base = (int)(__umul24(__umul24((unsigned)n, (unsigned)d.hp) + (unsigned)(ho * d.sh), (unsigned)d.wp) +
                              (unsigned)(wo * d.sw)) << lgcp;
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        fb[s][j] = *reinterpret_cast<const v4i*>(x + (doff[s] >= 0 ? base + doff[s] : d.zero_off));
+      for (int s = 0; s < KS; ++s) {
+        if (QNN_ABLATE == 1) fb[s][j] = (v4i){base, s, 1, 2};
+        else fb[s][j] = *reinterpret_cast<const v4i*>(x + (doff[s] >= 0 ? base + doff[s] : d.zero_off));
+      }
     }
   };
   v4i fnx[KS][TN];
   int nn[TN], nho[TN], nwo[TN];
   int pt = blockIdx.x / nby;
-  load_b(pt, fnx, nn, nho, nwo);
+  if constexpr (C::PF) load_b(pt, fnx, nn, nho, nwo);
   // border classes in LDS past the epilogue data: hcls[ho] * nwc, then wcls[wo]
   int* s_hc = reinterpret_cast<int*>(smem + p.scr_off);
   for (int i = tid; i < d.ho + d.wo; i += C::NT)
@@ -128,13 +137,17 @@ __global__ __launch_bounds__(C::NT) void qconv_direct_kernel(const int8_t* __res
   for (; pt < npt; pt += pstep) {
     v4i fb[KS][TN];
     int cn[TN], cho[TN], cwo[TN];
+    if constexpr (C::PF) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      cn[j] = nn[j], cho[j] = nho[j], cwo[j] = nwo[j];
+      for (int j = 0; j < TN; ++j) {
+        cn[j] = nn[j], cho[j] = nho[j], cwo[j] = nwo[j];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) fb[s][j] = fnx[s][j];
+        for (int s = 0; s < KS; ++s) fb[s][j] = fnx[s][j];
+      }
+      load_b(pt + pstep, fnx, nn, nho, nwo);  // the next tile's fragments land under this one's epilogue
+    } else {
+      load_b(pt, fb, cn, cho, cwo);  // (no prefetch: the co-resident waves hide the latency)
     }
-    load_b(pt + pstep, fnx, nn, nho, nwo);  // the next tile's fragments land under this one's epilogue
     v4i acc[TM][TN], sacc[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -146,6 +159,12 @@ __global__ __launch_bounds__(C::NT) void qconv_direct_kernel(const int8_t* __res
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
+        if (QNN_ABLATE == 2) {
+          sacc[j][0] += fb[s][j].x;
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[i][j][i & 3] ^= fa[s][i].y + fb[s][j].z;
+          continue;
+        }
         sacc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s][j], sacc[j], 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -161,6 +180,17 @@ __global__ __launch_bounds__(C::NT) void qconv_direct_kernel(const int8_t* __res
       P.n = cn[j], P.ho = cho[j], P.wo = cwo[j];
       pc = s_hc[P.ho] + s_hc[d.ho + P.wo];
     };
+    if (QNN_ABLATE == 3) {
+      int z = sumq[0] ^ cn[0];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z ^= acc[i][j][r];
+      if (z == 0x7fffffff) p.e.out_code0[0] = 1;
+      continue;
+    }
     q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, 0, lane, 1);
   }
 }
@@ -218,11 +248,16 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
 
 template <class C, int EK, bool MASKED>
 static int launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  switch ((p.taps * (p.d.cp >> 4) + 3) >> 2) {  // K steps holding real chunks
-    case 1: return launch<C, EK, MASKED, 1>(x, w, p, s, occ);
-    case 2: return launch<C, EK, MASKED, 2>(x, w, p, s, occ);
-    case 3: return launch<C, EK, MASKED, 3>(x, w, p, s, occ);
-    default: return launch<C, EK, MASKED, 4>(x, w, p, s, occ);
+  if constexpr (C::K576) {  // the K = 576 configurations: nine K steps, weights resident in VGPRs
+    if constexpr (MASKED) return arg_error("tile configuration not built for this layer / epilogue kind");
+    else return launch<C, EK, false, KS_3X3>(x, w, p, s, occ);
+  } else {
+    switch ((p.taps * (p.d.cp >> 4) + 3) >> 2) {  // K steps holding real chunks
+      case 1: return launch<C, EK, MASKED, 1>(x, w, p, s, occ);
+      case 2: return launch<C, EK, MASKED, 2>(x, w, p, s, occ);
+      case 3: return launch<C, EK, MASKED, 3>(x, w, p, s, occ);
+      default: return launch<C, EK, MASKED, 4>(x, w, p, s, occ);
+    }
   }
 }
 
@@ -247,15 +282,21 @@ static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStrea
 //   0   32 x 256            4 (32 x 64)        MobileNet's 32-channel stem, 32-channel 1x1s
 //   1   64 x 128            4 (64 x 32)        ResNet's 64-channel stem, 64-channel 1x1s
 //   2   128 x 64            4 (128 x 16)       128-channel 1x1s (MobileNet's pointwise layers)
+//   3   64 x 64             4 (64 x 16)        3x3 on 64 input channels (K = 576: ResNet layer 1):
+//                                              36 weight fragments resident per lane
+//   4   64 x 64             4 (64 x 16)        the same without the next-tile prefetch (<= 256 registers:
+//                                              two waves/SIMD hide each other's loads)
 using D0 = Cfg<2, 4>;
 using D1 = Cfg<4, 2>;
 using D2 = Cfg<8, 1>;
-constexpr int ND = 3;
+using D3 = Cfg<4, 1, true>;
+using D4 = Cfg<4, 1, true, false>;
+constexpr int ND = 5;
 struct Info {
   int bm, bn, acc_tiles;
   float rate;
 };
-static const Info INFO[ND] = {{32, 256, 8, 1.0f}, {64, 128, 8, 1.0f}, {128, 64, 8, 1.0f}};
+static const Info INFO[ND] = {{32, 256, 8, 1.0f}, {64, 128, 8, 1.0f}, {128, 64, 8, 1.0f}, {64, 64, 4, 1.0f}, {64, 64, 4, 1.0f}};
 
 }  // namespace dk
 
@@ -269,8 +310,12 @@ void direct_tile(int k, int* bm, int* bn) {
 bool direct_ok(int k, const Params& p) {
   if (k < 0 || k >= dk::ND) return false;
   const qnn_conv_desc& d = p.d;
-  if (d.kpad > dk::KPAD_MAX || d.kpad % 64 || d.cp % 16 || d.cout % 16) return false;
-  if (p.taps * d.cp > d.kpad || p.M >= (1 << 24)) return false;  // fdivmod's range
+  if (d.cp % 16 || d.cout % 16 || p.taps * d.cp > d.kpad || p.M >= (1 << 24)) return false;  // fdivmod's range
+  if (k >= 3) {  // exactly nine K steps of real chunks, no K mask
+    if (d.kmask || p.taps * d.cp != 64 * dk::KS_3X3) return false;
+  } else if (d.kpad > dk::KPAD_MAX || d.kpad % 64) {
+    return false;
+  }
   const int bm = dk::INFO[k].bm < 64 ? 64 : dk::INFO[k].bm;
   return dk::epi_bytes(p, bm) + 16 + 4 * (d.ho + d.wo) <= LDS_MAX;
 }
@@ -297,7 +342,9 @@ int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipS
   switch (k) {
     case 0: return dk::launch_ek<dk::D0>(x, w, p, s, occ);
     case 1: return dk::launch_ek<dk::D1>(x, w, p, s, occ);
-    default: return dk::launch_ek<dk::D2>(x, w, p, s, occ);
+    case 2: return dk::launch_ek<dk::D2>(x, w, p, s, occ);
+    case 3: return dk::launch_ek<dk::D3>(x, w, p, s, occ);
+    default: return dk::launch_ek<dk::D4>(x, w, p, s, occ);
   }
 }
 

@@ -89,7 +89,7 @@ def test_tile_kernel_families(lib):
     # families are contiguous id ranges, direct-fragment last
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
     assert len(runs) == len(set(runs)) + 1  # the ring family is split by the ping-pong ids 6-9
-    assert fams[-1] == "qconv_direct_kernel" and len(_lib.tile_ids("qconv_direct_kernel")) == 3
+    assert fams[-1] == "qconv_direct_kernel" and len(_lib.tile_ids("qconv_direct_kernel")) == 5
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 

@@ -133,6 +133,11 @@ DIRECT_SHAPES = [  # (name, direct-fragment configuration index, cin, cout, k, s
     ("mbn_stem_s2d_3x3_32_b256", 0, 3, 32, 3, 2, 1, 256, 224),
     ("r_stem_s2d_7x7_64_b128", 1, 3, 64, 7, 2, 3, 128, 224),
     ("pw_1x1_64_128_56_b256", 2, 64, 128, 1, 1, 0, 256, 56),
+    # K = 576 (3x3 on 64 channels, weights resident in VGPRs): ResNet layer 1 and the
+    # stride-2 entry of layer 2, at the ResNet-18 bench batch
+    ("r18_3x3_64_56_b128", 3, 64, 64, 3, 1, 1, 128, 56),
+    ("r18_3x3_64_56_b128_noprefetch", 4, 64, 64, 3, 1, 1, 128, 56),
+    ("r18_3x3_s2_64_128_b128", 3, 64, 128, 3, 2, 1, 128, 56),
 ]
 
 
