@@ -256,20 +256,25 @@ def main():
 
     elapsed = timed_run(step, args.steps, args.warmup, world, torch.cuda.synchronize)
 
-    # Per-launch HIP-event timing of every kernel of one forward (eager pass over the
-    # same launch sequence the graph replays; events on the launch stream)
-    names = sorted(set(engine.launch_names))
-    timer = _lib.LaunchTimer(names)
-    _lib.set_timer(timer)
-    reps = 3
-    with torch.no_grad():
-        for _ in range(reps):
-            engine._run_ops()
-    _lib.set_timer(None)
-    d = timer.durations_ms()
+    # Per-launch HIP-event timing of every kernel of one forward: each launch of the list the
+    # graph replays runs `reps` times back to back between two events on the launch stream
+    # (torch's current stream, which every qnn call is issued on), so the per-call host
+    # dispatch gap is amortised as in the replay and the figure is the kernel's own duration
+    # (the rocprofv3 kernel trace of the same launches agrees: profiles/r3_layers_*.json)
+    reps = 10
     per_kernel = {}
-    for n, ms in d:
-        per_kernel[n] = per_kernel.get(n, 0.0) + ms / reps
+    st = _lib.stream_of(engine.input)
+    with torch.no_grad():
+        engine._run_ops()
+        for op, name in zip(engine.ops, engine.launch_names):
+            op(st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                op(st)
+            e1.record()
+            e1.synchronize()
+            per_kernel[name] = per_kernel.get(name, 0.0) + e0.elapsed_time(e1) / reps
     conv_ms_per_fwd = per_kernel.get("qnn_qconv2d_fwd", 0.0) + per_kernel.get("qnn_qconv2d_maxpool_fwd", 0.0)
     launches = engine.num_launches
 

@@ -57,7 +57,7 @@ __device__ __forceinline__ void fdivmod(int m, int D, float invD, int& q, int& r
 }
 
 template <class C, int EK, bool MASKED, int KS>
-__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::PF ? 1 : 2))) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu((C::PF || C::TN > 1) ? 1 : 2))) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                             const Params p) {
   constexpr int TM = C::TM, TN = C::TN, CB = C::CB, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -286,6 +286,8 @@ static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStrea
 //                                              36 weight fragments resident per lane
 //   4   64 x 64             4 (64 x 16)        the same without the next-tile prefetch (<= 256 registers:
 //                                              two waves/SIMD hide each other's loads)
+// (two pixel tiles per wave, with or without the prefetch -- 400 / 256+spill registers, one wave per
+// SIMD -- measured 42-44 us on the ResNet-18 b128 layer-1 LUT launches: not kept)
 using D0 = Cfg<2, 4>;
 using D1 = Cfg<4, 2>;
 using D2 = Cfg<8, 1>;

@@ -3,6 +3,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "qnn_internal.h"
 
 namespace qnn {
@@ -175,6 +177,73 @@ __global__ __launch_bounds__(256) void quantize_s2d_kernel(const float* __restri
         if (ci < c && ok[uv])
           out.b[uv * c + ci] = (int8_t)((int)quant_code_fast(v[uv * 4 + ci], neg_min, scale, inv, qmax) - 128);
     *reinterpret_cast<int4*>(z + i * 16) = out.q;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 8)
+    *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
+}
+
+// The same space-to-depth codes, two s2d pixels (four input columns) per thread, for w % 4 == 0
+// and a 16-byte aligned x: every input row segment is read as the two aligned float4s around
+// it (a whole wave instruction = 1 KiB contiguous; the neighbour's shared float4 hits L1), so
+// the reads are 16 bytes per lane instead of 4 at a 2-float stride; each code byte is
+// quant_code_fast of the same float, so the codes are bitwise quantize_s2d_kernel's.
+// OFF = (4 - pad % 4) % 4: where column 4k - pad sits in its float4; CH = c (compile-time, so
+// every code byte's position is too and nothing goes through scratch)
+template <int OFF, int CH>
+__global__ __launch_bounds__(256) void quantize_s2d_x2_kernel(const float* __restrict__ x, int8_t* __restrict__ z,
+                                                              int n, int h, int w, int pad, int hz, int wz,
+                                                              float neg_min, float scale, float qmax) {
+  constexpr int c = CH;
+  const float inv = 1.0f / scale;
+  const int wz2 = (wz + 1) >> 1;
+  const int64_t total = (int64_t)n * hz * wz2;
+  const int64_t hw = (int64_t)h * w;
+  constexpr int off = OFF;  // column 4k - pad = 4a + off, a = floor((4k - pad) / 4)
+  const int w4 = w >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % wz2);
+    const int64_t r = i / wz2;
+    const int h2 = (int)(r % hz), img = (int)(r / hz);
+    const int a = (4 * k - pad - off) >> 2;  // exact: 4k - pad - off is a multiple of 4
+    float v[2][4][4];                        // [row][channel][column 0..3 = 4k - pad ..]
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int iy = 2 * h2 + rr - pad;
+      const bool rok = iy >= 0 && iy < h;
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) {
+        float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+        if (ci < c && rok) {
+          const float4* row = reinterpret_cast<const float4*>(x + ((int64_t)img * c + ci) * hw + (int64_t)iy * w);
+          if (a >= 0 && a < w4) A = row[a];
+          if (a + 1 >= 0 && a + 1 < w4) B = row[a + 1];
+        }
+        const float e[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[rr][ci][j] = e[off + j];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int w2 = 2 * k + p;
+      if (w2 >= wz) break;
+      union {
+        int8_t b[16];
+        int4 q;
+      } out;
+      out.q = make_int4(0, 0, 0, 0);
+#pragma unroll
+      for (int uv = 0; uv < 4; ++uv) {
+        const int rr = uv >> 1, u = uv & 1;
+        const int iy = 2 * h2 + rr - pad, ix = 2 * w2 + u - pad;
+        const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci)
+          if (ci < c && ok)
+            out.b[uv * c + ci] = (int8_t)((int)quant_code_fast(v[rr][ci][2 * p + u], neg_min, scale, inv, qmax) - 128);
+      }
+      *reinterpret_cast<int4*>(z + (r * wz + w2) * 16) = out.q;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x < 8)
     *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
@@ -432,8 +501,28 @@ int qnn_quantize_nchw_to_s2d8(const float* x, int8_t* z, int n, int c, int h, in
   QNN_REQUIRE(z && (n == 0 || x), "null pointer");
   QNN_REQUIRE((((uintptr_t)z) & 15) == 0, "z must be 16-byte aligned");
   const int64_t total = (int64_t)n * hz * wz;
-  hipLaunchKernelGGL(quantize_s2d_kernel, dim3(grid_for(total > 0 ? total : 1, 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, z, n, c, h, w, pad, hz, wz, neg_min, scale, qmax);
+  if (w % 4 == 0 && (((uintptr_t)x) & 15) == 0) {
+    const int64_t pairs = (int64_t)n * hz * ((wz + 1) / 2);
+    const dim3 grid(grid_for(pairs > 0 ? pairs : 1, 256));
+    auto go = [&](auto offc) {
+      constexpr int O = decltype(offc)::value;
+      switch (c) {
+        case 1: hipLaunchKernelGGL((quantize_s2d_x2_kernel<O, 1>), grid, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+        case 2: hipLaunchKernelGGL((quantize_s2d_x2_kernel<O, 2>), grid, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+        case 3: hipLaunchKernelGGL((quantize_s2d_x2_kernel<O, 3>), grid, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+        default: hipLaunchKernelGGL((quantize_s2d_x2_kernel<O, 4>), grid, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+      }
+    };
+    switch ((4 - (pad & 3)) & 3) {
+      case 0: go(std::integral_constant<int, 0>{}); break;
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      default: go(std::integral_constant<int, 3>{}); break;
+    }
+  } else {
+    hipLaunchKernelGGL(quantize_s2d_kernel, dim3(grid_for(total > 0 ? total : 1, 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, z, n, c, h, w, pad, hz, wz, neg_min, scale, qmax);
+  }
   QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_s2d8");
   return QNN_OK;
 }

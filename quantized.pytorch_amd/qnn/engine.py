@@ -73,13 +73,21 @@ class Engine:
     the model's device).  `engine.input` is a static input buffer; passing it (or
     nothing) avoids the copy.  graph=False runs the launches eagerly (debugging)."""
 
-    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None, fuse_stem_pool=True):
+    def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None, fuse_stem_pool=True,
+                 max_links=None):
         """tile=k forces tile configuration k on every contraction it is built for (the
         others keep the cost model's choice); tile=None autotunes (or the cost model
         when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile.
         fuse_stem_pool: the ResNet stem conv and its max-pool as one launch
-        (qnn_qconv2d_maxpool_fwd) where the shapes allow; False keeps two launches."""
+        (qnn_qconv2d_maxpool_fwd) where the shapes allow; False keeps two launches.
+        max_links: the longest residual code chain (0 .. QNN_MAX_RES; 0 = every block
+        output an fp32 map); None = QNN_ENGINE_MAX_LINKS or QNN_MAX_RES."""
         self.fuse_stem_pool = fuse_stem_pool
+        if max_links is None:
+            max_links = int(os.environ.get("QNN_ENGINE_MAX_LINKS", _lib.MAX_RES))
+        if not 0 <= max_links <= _lib.MAX_RES:
+            raise ValueError(f"qnn.Engine: max_links must be in 0..{_lib.MAX_RES}")
+        self.max_links = int(max_links)
         if model.training:
             raise RuntimeError("qnn.Engine: call model.eval() first (the engine is the eval forward)")
         self.model = model
@@ -440,7 +448,7 @@ class Engine:
         bnc = None
         if nxt is not None and nxt.downsample is None:  # the next block adds this output
             f32c, links, relu0 = chain
-            if len(links) < _lib.MAX_RES:
+            if len(links) < self.max_links:
                 bnc = self._btiled(Ho, Wo, cout)
                 out.res = (f32c, links + [(bnc, last_bn)], relu0)
             else:

@@ -97,3 +97,19 @@ def test_engine_launch_count_resnet18(gpu):
     assert eng.launch_names.count("qnn_qconv2d_maxpool_fwd") == 1
     y = eng()
     assert torch.isfinite(y).all()
+
+
+@pytest.mark.parametrize("max_links", [0, 1, 2, 3])
+@pytest.mark.parametrize("name", ["resnet18_imagenet", "resnet50_imagenet"])
+def test_engine_chain_length_bitwise(gpu, name, max_links):
+    """Every residual chain limit (0 = an fp32 map at every identity shortcut) gives the
+    same feature map entering the head as the module path, bitwise: the chain links
+    recompute the fp32 block inputs with their producers' exact ops."""
+    d = load_fixture("model_" + name)
+    model, x = build_model(d)
+    model = model.to(gpu)
+    xg = x.to(gpu)
+    _, mod_feat = _module_path(model, xg)
+    eng = Engine(model, batch=x.shape[0], max_links=max_links)
+    eng(xg)
+    assert torch.equal(eng.head_input, mod_feat.permute(0, 2, 3, 1)), f"max_links={max_links}: != module path"

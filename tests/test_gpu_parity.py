@@ -90,11 +90,16 @@ def test_activation_codes_padded_nhwc8(gpu, shape, c_pad, pad):
     assert np.all(q[nbytes:].cpu().numpy() == 0)                 # zero page
 
 
-def test_activation_codes_space_to_depth(gpu):
-    N, C, H, W, pad = 2, 3, 37, 30, 3
+@pytest.mark.parametrize("H,W,pad,hz,wz", [
+    (37, 30, 3, 21, 18),     # w % 4 != 0: one s2d pixel per thread
+    (36, 32, 3, 20, 19),     # w % 4 == 0: two per thread (aligned float4 pairs), 7x7/2 stem padding, odd wz
+    (36, 32, 1, 18, 17),     # MobileNet's 3x3/2 stem padding
+    (40, 40, 2, 22, 22),     # even padding
+])
+def test_activation_codes_space_to_depth(gpu, H, W, pad, hz, wz):
+    N, C = 2, 3
     x = synthetic.input_batch((N, C, H, W), 6)
     mn, mx = -2.0, 2.5
-    hz, wz = 21, 18
     z = torch.full((N * hz * wz * 16 + 128,), 55, dtype=torch.int8, device=gpu)
     xd = x.to(gpu)
     _lib.call("qnn_quantize_nchw_to_s2d8", _lib.ptr(xd), _lib.ptr(z), N, C, H, W, pad, hz, wz, -mn,
