@@ -5,8 +5,19 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "qconv_common.h"
+
+#ifndef QNN_DW_PF
+#define QNN_DW_PF 1  // depthwise: 1 = next group's loads in flight under this one (register double buffer)
+#endif
+#ifndef QNN_DW_WPE
+#define QNN_DW_WPE 2  // depthwise: waves per SIMD the register budget is sized for
+#endif
+#ifndef QNN_DW_P
+#define QNN_DW_P 4  // depthwise: channel pairs per thread (4: 8 channels, 8-byte loads; 2: 4 channels)
+#endif
 
 namespace qnn {
 
@@ -214,30 +225,34 @@ __global__ void dwconv_fused_kernel(const int8_t* __restrict__ x, int n, int h, 
 // and feeds up to 3 outputs from registers; the 9x8 tap weights, the bias and the
 // RangeBN vectors live in registers; both quantizers run division-free
 // (quant_code_fast, bit-identical); no 64-bit index arithmetic.
-template <int S, int R>
-__global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__ x, int h, int w, int pad, int hp,
+template <int S, int R, int P>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE))) void dwconv3_kernel(const int8_t* __restrict__ x, int h, int w, int pad, int hp,
                                                       int wp, int cp, int c, const float* __restrict__ wt, int ho,
                                                       int wo, float x_min, float x_scale, const float* bias,
                                                       qnn_bn_params bn, float bn_inv, int has_bn, int relu,
                                                       float* out_f32, qnn_code_out c0, float c0_inv, int rows) {
-  constexpr int K = 3, NCOL = (R - 1) * S + K;
-  const int ct = c >> 3, per_blk = 256 / ct;
+  constexpr int K = 3, NCOL = (R - 1) * S + K, CPT = 2 * P;  // CPT channels per thread
+  using LT = std::conditional_t<P == 4, uint2, uint32_t>;    // one tap of them: 8 or 4 code bytes
+  const int ct = c / CPT, per_blk = 256 / ct;
   const int tc = threadIdx.x % ct, tp = threadIdx.x / ct;
-  if (tp >= per_blk) return;  // c/8 not a divisor of 256: idle tail threads
-  const int nxg = (wo + R - 1) / R, total = rows * nxg, cb = 8 * tc;
+  if (tp >= per_blk) return;  // c/CPT not a divisor of 256: idle tail threads
+  const int nxg = (wo + R - 1) / R, total = rows * nxg, cb = CPT * tc;
   if (blockIdx.x * per_blk + tp >= total) return;
   // every per-channel quantity as packed pairs (channels 2p, 2p+1): v_pk_fma/mul/add run the
   // same IEEE fp32 op per element as the scalar form, so the results are bitwise unchanged
-  f2 wv[K * K][4];
+  f2 wv[K * K][P];
 #pragma unroll
   for (int t = 0; t < K * K; ++t) {
     const float4 a = *reinterpret_cast<const float4*>(wt + t * c + cb);
-    const float4 b = *reinterpret_cast<const float4*>(wt + t * c + cb + 4);
-    wv[t][0] = (f2){a.x, a.y}, wv[t][1] = (f2){a.z, a.w}, wv[t][2] = (f2){b.x, b.y}, wv[t][3] = (f2){b.z, b.w};
+    wv[t][0] = (f2){a.x, a.y}, wv[t][1] = (f2){a.z, a.w};
+    if constexpr (P == 4) {
+      const float4 b = *reinterpret_cast<const float4*>(wt + t * c + cb + 4);
+      wv[t][2] = (f2){b.x, b.y}, wv[t][3] = (f2){b.z, b.w};
+    }
   }
-  f2 bi[4], mean[4], sq[4], wq[4], bq[4];
+  f2 bi[P], mean[P], sq[P], wq[P], bq[P];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < P; ++p) {
     bi[p] = bias ? (f2){bias[cb + 2 * p], bias[cb + 2 * p + 1]} : (f2){0.f, 0.f};
     if (has_bn) {
       mean[p] = (f2){bn.mean[cb + 2 * p], bn.mean[cb + 2 * p + 1]};
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
   // oy*S + r and column < wp) and all K x NCOL issued together -- a load under a branch
   // gets its own vmcnt(0) wait.  Software-pipelined: the next group's loads are in flight
   // while this group computes.
-  auto load = [&](int g, uint2 (&v)[K][NCOL]) {
+  auto load = [&](int g, LT (&v)[K][NCOL]) {
     const int row = g / nxg, xg = g - row * nxg;
     const int img = row / ho, oy = row - img * ho;
     const int8_t* xrow = x + ((size_t)img * hp + oy * S) * wp * cp + cb;
@@ -264,25 +279,26 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
 #pragma unroll
       for (int col = 0; col < NCOL; ++col) {
         const int px = min(xg * R * S + col, wp - 1);
-        v[r][col] = *reinterpret_cast<const uint2*>(xrow + ((size_t)r * wp + px) * cp);
+        v[r][col] = *reinterpret_cast<const LT*>(xrow + ((size_t)r * wp + px) * cp);
       }
   };
   // grid-stride over (row, R-pixel group): the register-resident parameters are loaded
   // once per thread and reused across all of its groups
   const int step = gridDim.x * per_blk;
-  uint2 v[K][NCOL];
-  load(blockIdx.x * per_blk + tp, v);
+  LT v[K][NCOL];
+  if (QNN_DW_PF) load(blockIdx.x * per_blk + tp, v);
   for (int pg = blockIdx.x * per_blk + tp; pg < total; pg += step) {
     const int row = pg / nxg, xg = pg - row * nxg;
     const int img = row / ho, oy = row - img * ho;
     const int ox0 = xg * R;
-    uint2 vn[K][NCOL];
-    load(min(pg + step, total - 1), vn);
-    f2 acc[R][4];
+    LT vn[K][NCOL];
+    if (QNN_DW_PF) load(min(pg + step, total - 1), vn);
+    else load(pg, v);
+    f2 acc[R][P];
 #pragma unroll
     for (int j = 0; j < R; ++j)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) acc[j][p] = (f2){0.f, 0.f};
+      for (int p = 0; p < P; ++p) acc[j][p] = (f2){0.f, 0.f};
 
 #pragma unroll
     for (int r = 0; r < K; ++r) {
@@ -292,18 +308,23 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
       for (int col = 0; col < NCOL; ++col) {
         const int px = ox0 * S + col;
         if (px < pad || px >= pad + w) continue;
-        const uint32_t lo = v[r][col].x ^ 0x80808080u, hi = v[r][col].y ^ 0x80808080u;  // code' ^ 0x80 = code
-        f2 xh[4];  // dequant(q) = q * s + min (quantize.py:100), pairs
+        uint32_t lo, hi = 0;  // code' ^ 0x80 = code
+        if constexpr (P == 4) lo = v[r][col].x ^ 0x80808080u, hi = v[r][col].y ^ 0x80808080u;
+        else lo = v[r][col] ^ 0x80808080u;
+        f2 xh[P];  // dequant(q) = q * s + min (quantize.py:100), pairs
         xh[0] = (f2){(float)(lo & 255), (float)((lo >> 8) & 255)} * xs2 + xm2;
         xh[1] = (f2){(float)((lo >> 16) & 255), (float)(lo >> 24)} * xs2 + xm2;
-        xh[2] = (f2){(float)(hi & 255), (float)((hi >> 8) & 255)} * xs2 + xm2;
-        xh[3] = (f2){(float)((hi >> 16) & 255), (float)(hi >> 24)} * xs2 + xm2;
+        if constexpr (P == 4) {
+          xh[2] = (f2){(float)(hi & 255), (float)((hi >> 8) & 255)} * xs2 + xm2;
+          xh[3] = (f2){(float)((hi >> 16) & 255), (float)(hi >> 24)} * xs2 + xm2;
+        }
+        (void)hi;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
           const int s = col - j * S;
           if (s < 0 || s >= K) continue;  // compile-time
 #pragma unroll
-          for (int p = 0; p < 4; ++p) acc[j][p] = pfma(xh[p], wv[r * K + s][p], acc[j][p]);
+          for (int p = 0; p < P; ++p) acc[j][p] = pfma(xh[p], wv[r * K + s][p], acc[j][p]);
         }
       }
     }
@@ -312,9 +333,9 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
     for (int j = 0; j < R; ++j) {
       const int ox = ox0 + j;
       if (ox >= wo) break;
-      f2 val[4];
+      f2 val[P];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < P; ++p) {
         f2 y = bias ? acc[j][p] + bi[p] : acc[j][p];
         if (has_bn) {  // bn_apply(quant_code(y)), quantize.py:488-499
           f2 o = rint2(qclamp2(y, bnp)) * bs2;
@@ -330,19 +351,25 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const int8_t* __restrict__
       if (out_f32) {
         float* o = out_f32 + (((size_t)img * ho + oy) * wo + ox) * c + cb;
         *reinterpret_cast<float4*>(o) = make_float4(val[0].x, val[0].y, val[1].x, val[1].y);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(val[2].x, val[2].y, val[3].x, val[3].y);
+        if constexpr (P == 4) *reinterpret_cast<float4*>(o + 4) = make_float4(val[2].x, val[2].y, val[3].x, val[3].y);
       }
       if (c0.ptr) {
+        int8_t* cp0 = c0.ptr + (((size_t)img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * c0.cp + cb;
         const int p0 = pack4(qclamp2(val[0], c0p) + MAGIC_S8, qclamp2(val[1], c0p) + MAGIC_S8);
-        const int p1 = pack4(qclamp2(val[2], c0p) + MAGIC_S8, qclamp2(val[3], c0p) + MAGIC_S8);
-        *reinterpret_cast<uint2*>(c0.ptr + (((size_t)img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * c0.cp + cb) =
-            make_uint2((uint32_t)p0, (uint32_t)p1);
+        if constexpr (P == 4) {
+          const int p1 = pack4(qclamp2(val[2], c0p) + MAGIC_S8, qclamp2(val[3], c0p) + MAGIC_S8);
+          *reinterpret_cast<uint2*>(cp0) = make_uint2((uint32_t)p0, (uint32_t)p1);
+        } else {
+          *reinterpret_cast<uint32_t*>(cp0) = (uint32_t)p0;
+        }
       }
     }
+    if (QNN_DW_PF) {
 #pragma unroll
-    for (int r = 0; r < K; ++r)
+      for (int r = 0; r < K; ++r)
 #pragma unroll
-      for (int col = 0; col < NCOL; ++col) v[r][col] = vn[r][col];
+        for (int col = 0; col < NCOL; ++col) v[r][col] = vn[r][col];
+    }
   }
 }
 
@@ -472,16 +499,17 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
   const qnn_code_out c0 = code0 ? *code0 : none_code();
   const char* fg = getenv("QNN_DW_GENERIC");  // read per call: tests compare both kernels bitwise
   const int force_generic = fg ? atoi(fg) : 0;
-  const bool fast = !force_generic && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) && c % 8 == 0 &&
-                    c / 8 <= 256 && cp % 8 == 0 && (((uintptr_t)x) & 7) == 0 && (((uintptr_t)w_hat_t) & 15) == 0 &&
+  constexpr int CPT = 2 * QNN_DW_P;
+  const bool fast = !force_generic && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) && c % CPT == 0 &&
+                    c / CPT <= 256 && cp % 8 == 0 && (((uintptr_t)x) & 7) == 0 && (((uintptr_t)w_hat_t) & 15) == 0 &&
                     (!out_f32 || (((uintptr_t)out_f32) & 15) == 0) &&
                     (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0));
   if (fast) {
     const int R = sh == 1 ? 4 : 2;  // stride 2: 2 pixels (5 input columns) per thread, register budget
-    const int rows = n * ho, ct = c / 8;
+    const int rows = n * ho, ct = c / CPT;
     const int64_t groups = (int64_t)rows * ((wo + R - 1) / R);
     QNN_REQUIRE(groups < (1LL << 31) && (int64_t)n * hp * wp * cp < (1LL << 40), "depthwise too large");
-    auto kern = sh == 1 ? dwconv3_kernel<1, 4> : dwconv3_kernel<2, 2>;
+    auto kern = sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P> : dwconv3_kernel<2, 2, QNN_DW_P>;
     // grid-stride, sized to the resident capacity (the loop is software-pipelined)
     static int num_cu = 0;
     if (!num_cu && hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) num_cu = 256;
