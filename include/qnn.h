@@ -61,6 +61,17 @@ int qnn_fake_quant_f32(const float* x, float* y, int64_t n, float neg_min, float
 int qnn_fake_quant_vec_f32(const float* x, float* y, int n, float qmax, int scale_mode,
                            float* range_out, qnn_stream_t stream);
 
+/* The gradient quantizer of training (quantize.py:123-139, UniformQuantizeGrad.backward):
+ * UniformQuantize().apply(grad, num_bits, min, max, stochastic, inplace) binds
+ * enforce_true_zero = True, so per element, in the reference's op order (:76-97):
+ *   t = g / scale; t = t + zero_point; [t = t + noise]; t = rint(clamp(t, 0, qmax));
+ *   out = (t - zero_point) * scale
+ * with scale = max((max - min) / qmax, 1e-8) and zero_point = int(clamp(-min / scale, 0, qmax))
+ * computed by the caller in double from the Python-float range, as the reference does.
+ * noise (nullable = not stochastic): the uniform(-0.5, 0.5) draw, one per element. */
+int qnn_grad_quant_f32(const float* g, const float* noise, float* out, int64_t n, float scale, float zero_point,
+                       float qmax, qnn_stream_t stream);
+
 /* UniformQuantize.forward with a tensor range per row (fp32 scale), as the
  * per-output-channel weight quantization of QConv2d/QLinear (quantize.py:332-334,
  * weight_min/max of shape (Cout,1,..)) and the generic `quantize(x, b, t_min, t_max)`:

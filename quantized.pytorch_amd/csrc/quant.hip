@@ -249,6 +249,22 @@ __global__ __launch_bounds__(256) void quantize_s2d_x2_kernel(const float* __res
     *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
+// ------------------------------------------------------------------ gradient quantizer
+// quantize.py:76-97 with enforce_true_zero (the binding of UniformQuantizeGrad.backward):
+// the reference's in-place op order, one element per lane, four per thread
+__global__ __launch_bounds__(256) void grad_quant_kernel(const float* __restrict__ g, const float* __restrict__ noise,
+                                                         float* __restrict__ out, int64_t n, float scale, float zp,
+                                                         float qmax) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float t = g[i] / scale;  // output.div_(scale)
+    t = t + zp;              // .add_(zero_point)
+    if (noise) t = t + noise[i];
+    t = rintf(fminf(fmaxf(t, 0.0f), qmax));  // clamp_(qmin, qmax).round_()
+    t = t + (-zp);                           // add_(-zero_point)
+    out[i] = t * scale;                      // .mul_(scale)
+  }
+}
+
 // ------------------------------------------------------------------ weight pack
 // One block per (padded) output channel.  Deterministic fp64 tap sums.
 __global__ __launch_bounds__(256) void pack_weight_kernel(const float* __restrict__ w, int cout, int cin_g, int kh,
@@ -477,6 +493,18 @@ int qnn_fake_quant_vec_f32(const float* x, float* y, int n, float qmax, int scal
   hipLaunchKernelGGL(fake_quant_vec_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, y, n, qmax, scale_mode,
                      range_out);
   QNN_LAUNCH_CHECK("qnn_fake_quant_vec_f32");
+  return QNN_OK;
+}
+
+int qnn_grad_quant_f32(const float* g, const float* noise, float* out, int64_t n, float scale, float zero_point,
+                       float qmax, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0, "n must be >= 0");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(g && out, "null pointer");
+  hipLaunchKernelGGL(grad_quant_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, g, noise, out, n,
+                     scale, zero_point, qmax);
+  QNN_LAUNCH_CHECK("qnn_grad_quant_f32");
   return QNN_OK;
 }
 

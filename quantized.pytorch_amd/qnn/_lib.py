@@ -70,6 +70,7 @@ SIGNATURES = {
     "qnn_fake_quant_f32": [c_ptr, c_ptr, c_i64, c_float, c_float, c_float, c_float, c_ptr],
     "qnn_fake_quant_rows_f32": [c_ptr, c_ptr, c_int, c_i64, c_ptr, c_ptr, c_float, c_ptr],
     "qnn_fake_quant_vec_f32": [c_ptr, c_ptr, c_int, c_float, c_int, c_ptr, c_ptr],
+    "qnn_grad_quant_f32": [c_ptr, c_ptr, c_ptr, ctypes.c_int64, c_float, c_float, c_float, c_ptr],
     "qnn_quantize_nchw_to_nhwc8": [c_ptr, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
                                    c_float, c_ptr],
     "qnn_quantize_nchw_to_s2d8": [c_ptr, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,

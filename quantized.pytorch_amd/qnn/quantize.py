@@ -64,9 +64,42 @@ def _round_up(a, b):
 
 
 # ============================================================ functional quantize
+class _Passthrough(torch.autograd.Function):
+    """A quantized value already computed on the device, with the straight-through gradient
+    to the tensor it quantizes (quantize.py:105-109)."""
+
+    @staticmethod
+    def forward(ctx, x, q):
+        return q.view_as(q)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _QuantizeSTE(torch.autograd.Function):
+    """UniformQuantize (quantize.py:39-109) under autograd: the device fake-quantizer
+    forward, the straight-through estimator backward (:105-109)."""
+
+    @staticmethod
+    def forward(ctx, x, num_bits, min_value, max_value, num_chunks):
+        return _quantize_fwd(x.detach(), num_bits, min_value, max_value, num_chunks)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output, None, None, None, None
+
+
 def quantize(x, num_bits=8, min_value=None, max_value=None, num_chunks=None, stochastic=False, inplace=False):
     """quantize.py:159-160 with its effective binding: `stochastic` is never set and
-    the asymmetric branch always runs.  GPU only."""
+    the asymmetric branch always runs.  GPU only.  Under autograd
+    (training) the gradient passes straight through (:105-109)."""
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _QuantizeSTE.apply(x, num_bits, min_value, max_value, num_chunks)
+    return _quantize_fwd(x, num_bits, min_value, max_value, num_chunks, inplace)
+
+
+def _quantize_fwd(x, num_bits=8, min_value=None, max_value=None, num_chunks=None, inplace=False):
     _require_device(x, "quantize()")
     qmax = _qmax(num_bits)
     xc = x.contiguous()
@@ -99,20 +132,134 @@ def quantize(x, num_bits=8, min_value=None, max_value=None, num_chunks=None, sto
     return out
 
 
+def grad_noise(like):
+    """The stochastic-rounding draw of the gradient quantizer: `output.new(output.shape)
+    .uniform_(-0.5, 0.5)` (quantize.py:92-94), on the gradient's device.  Module-level so a
+    test can substitute a fixed draw (GRAD_NOISE[0])."""
+    return torch.empty_like(like).uniform_(-0.5, 0.5)
+
+
+GRAD_NOISE = [grad_noise]
+
+
+def quantize_grad_tensor(g, num_bits=8, min_value=None, max_value=None, stochastic=True):
+    """UniformQuantizeGrad.backward (quantize.py:123-139) on a gradient tensor: the range
+    from the gradient as Python floats, then UniformQuantize().apply(grad, num_bits, min, max,
+    stochastic, inplace) -- which binds enforce_true_zero=True (:41-43), so the zero point is
+    integral (:76-87) -- on the device (qnn_grad_quant_f32)."""
+    _require_device(g, "quantize_grad")
+    gc = g.contiguous()
+    mn = float(gc.min()) if min_value is None else float(min_value)
+    mx = float(gc.max()) if max_value is None else float(max_value)
+    qmin, qmax = 0.0, 2.0 ** num_bits - 1.0
+    scale = max((mx - mn) / (qmax - qmin), 1e-8)
+    izp = qmin - mn / scale
+    zp = int(qmin if izp < qmin else (qmax if izp > qmax else izp))
+    noise = GRAD_NOISE[0](gc).contiguous() if stochastic else None
+    out = torch.empty_like(gc)
+    _lib.call("qnn_grad_quant_f32", _lib.ptr(gc), _lib.ptr(noise), _lib.ptr(out), gc.numel(),
+              float(np.float32(scale)), float(zp), qmax, _lib.stream_of(gc))
+    return out
+
+
+class _QuantizeGrad(torch.autograd.Function):
+    """UniformQuantizeGrad (quantize.py:112-139): identity forward, quantized gradient."""
+
+    @staticmethod
+    def forward(ctx, x, num_bits, min_value, max_value, stochastic):
+        ctx.args = (num_bits, min_value, max_value, stochastic)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return quantize_grad_tensor(grad_output, *ctx.args), None, None, None, None
+
+
 def quantize_grad(x, num_bits=8, min_value=None, max_value=None, stochastic=True, inplace=False):
-    """UniformQuantizeGrad (quantize.py:112-121, :163-164): identity in forward."""
+    """UniformQuantizeGrad (quantize.py:112-121, :163-164): identity in forward; under
+    autograd the backward quantizes the incoming gradient (quantize_grad_tensor)."""
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _QuantizeGrad.apply(x, num_bits, min_value, max_value, stochastic)
     return x
 
 
 def conv2d_biprec(input, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, num_bits_grad=None):
-    """quantize.py:142-148.  The forward value out1 + out2 - out1 equals one conv
-    bitwise; kept for API completeness (float operands)."""
-    return F.conv2d(input, weight, bias, stride, padding, dilation, groups)
+    """quantize.py:142-148: out1 (input detached) carries the weight/bias gradient, out2
+    (weight/bias detached) the input gradient through the gradient quantizer; the forward
+    value out1 + out2 - out1 is one conv bitwise."""
+    out1 = F.conv2d(input.detach(), weight, bias, stride, padding, dilation, groups)
+    out2 = F.conv2d(input, weight.detach(), bias.detach() if bias is not None else None, stride, padding, dilation,
+                    groups)
+    out2 = quantize_grad(out2, num_bits=num_bits_grad)
+    return out1 + out2 - out1.detach()
 
 
 def linear_biprec(input, weight, bias=None, num_bits_grad=None):
-    """quantize.py:151-156 (forward value == one linear)."""
-    return F.linear(input, weight, bias)
+    """quantize.py:151-156."""
+    out1 = F.linear(input.detach(), weight, bias)
+    out2 = F.linear(input, weight.detach(), bias.detach() if bias is not None else None)
+    out2 = quantize_grad(out2, num_bits=num_bits_grad)
+    return out1 + out2 - out1.detach()
+
+
+class _QLayerTrain(torch.autograd.Function):
+    """The training forward of QConv2d / QLinear (quantize.py:314-354, :398-432): the int8
+    MFMA forward (bitwise the eval kernel's output for the same ranges), and the backward
+    autograd derives from the reference's graph --
+      input_  = quantize_input(input)          straight-through (:105-109)
+      qweight = quantize(weight, w_min, w_max) straight-through
+      qbias   = quantize(bias, b_min, b_max)   straight-through
+      output  = F.conv2d(input_, qweight, qbias)                 [num_bits_grad None]
+              = quantize_grad(F.conv2d(...))                     [num_bits_grad, no biprecision]
+              = conv2d_biprec(...)                               [num_bits_grad and biprecision]
+    so grad_input = conv_input(qweight, g_in), grad_weight = conv_weight(input_, g_w),
+    grad_bias = sum(g_w), with g_in = g_w = the (possibly quantized) output gradient, except
+    under biprecision where only g_in is quantized.  The transposed contractions are fp32
+    (torch's conv backward); only the quantization semantics are this row's."""
+
+    @staticmethod
+    def forward(ctx, input, weight, bias, mod, rng, fwd):
+        ctx.mod, ctx.rng = mod, rng
+        ctx.save_for_backward(input, weight, bias)
+        with torch.no_grad():
+            return fwd(input.detach())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, b = ctx.saved_tensors
+        mod = ctx.mod
+        gy = gy.contiguous()
+        g_in = g_w = gy
+        if mod.num_bits_grad is not None:
+            gq = quantize_grad_tensor(gy, mod.num_bits_grad)
+            g_in = gq
+            if not mod.biprecision:
+                g_w = gq
+        with torch.no_grad():
+            xh = _quantize_fwd(x.detach().contiguous(), mod.num_bits, ctx.rng[0], ctx.rng[1])
+            wh = _quantize_fwd(w.detach().contiguous(), mod.num_bits_weight, mod.weight_min, mod.weight_max)
+            gx = gw = gb = None
+            if isinstance(mod, nn.Conv2d):
+                args = (mod.stride, mod.padding, mod.dilation, mod.groups)
+                if ctx.needs_input_grad[0]:
+                    gx = torch.nn.grad.conv2d_input(x.shape, wh, g_in, *args)
+                if ctx.needs_input_grad[1]:
+                    gw = torch.nn.grad.conv2d_weight(xh, w.shape, g_w, *args)
+                if b is not None and ctx.needs_input_grad[2]:
+                    gb = g_w.sum((0, 2, 3))
+            else:
+                if ctx.needs_input_grad[0]:
+                    gx = g_in @ wh
+                if ctx.needs_input_grad[1]:
+                    gw = g_w.reshape(-1, g_w.shape[-1]).t() @ xh.reshape(-1, xh.shape[-1])
+                if b is not None and ctx.needs_input_grad[2]:
+                    gb = g_w.reshape(-1, g_w.shape[-1]).sum(0)
+        return gx, gw, gb, None, None, None
+
+
+def _needs_grad(input, mod):
+    return torch.is_grad_enabled() and (input.requires_grad or mod.weight.requires_grad or
+                                        (mod.bias is not None and mod.bias.requires_grad))
 
 
 # ============================================================ QuantNode / QuantMeasure
@@ -543,13 +690,19 @@ class QConv2d(nn.Conv2d, QuantNode, _QLayerMixin):
             raise NotImplementedError("qnn: dilation != 1 is not on the int8 path")
         if self.padding_mode != "zeros" or isinstance(self.padding, str):
             raise NotImplementedError("qnn: only explicit zero padding is on the int8 path")
-        x = input.detach().contiguous()
-        with torch.no_grad():
+        if self.groups != 1 and not self._is_depthwise():
+            raise NotImplementedError("qnn: grouped conv other than depthwise is not on the int8 path")
+
+        def fwd(x):
+            x = x.contiguous()
             if self._is_depthwise():
                 return self._dw_forward(x, rng)
-            if self.groups != 1:
-                raise NotImplementedError("qnn: grouped conv other than depthwise is not on the int8 path")
             return self._int8_forward(x, rng, self.stride, self.padding)
+
+        if _needs_grad(input, self):  # training (§8(f4)): the same forward, the reference's backward
+            return _QLayerTrain.apply(input, self.weight, self.bias, self, rng, fwd)
+        with torch.no_grad():
+            return fwd(input.detach())
 
     def _dw_forward(self, x, rng):
         pk = self._pack(depthwise=True)
@@ -615,10 +768,16 @@ class QLinear(nn.Linear, QuantNode, _QLayerMixin):
             return F.linear(input, self.weight, self.bias)
         _require_device(input, "QLinear")
         lead = input.shape[:-1]
-        x = input.detach().reshape(-1, input.shape[-1]).contiguous()
-        with torch.no_grad():
+
+        def fwd(x):
+            x = x.reshape(-1, input.shape[-1]).contiguous()
             y = self._int8_forward(x.view(x.shape[0], x.shape[1], 1, 1), rng, (1, 1), (0, 0))
-        return y.view(*lead, self.out_features)
+            return y.view(*lead, self.out_features)
+
+        if _needs_grad(input, self):  # training (§8(f4))
+            return _QLayerTrain.apply(input, self.weight, self.bias, self, rng, fwd)
+        with torch.no_grad():
+            return fwd(input.detach())
 
 
 # ============================================================ RangeBN
@@ -702,12 +861,22 @@ class RangeBN(nn.Module):
 
     def _forward_reference_ops(self, x):
         """Train / measure-mode branch with torch ops (quantize.py:461-505)."""
+        grad = torch.is_grad_enabled() and (x.requires_grad or any(
+            p is not None and p.requires_grad for p in (self.weight, self.bias)))
         x = self.quantize_input(x)
         if x.dim() == 2:
             x = x.unsqueeze(-1).unsqueeze(-1)
         if self.training:
-            # the chunked reductions in one device pass (qnn_rangebn_stats_f32), the rest op for op
-            mean_max, mean_min, mean, n = rangebn_stats(x, self.num_chunks)
+            if grad:  # training (§8(f4)): the statistics as the reference's differentiable torch ops
+                B, C, H, W = x.shape
+                y = x.transpose(0, 1).contiguous().view(C, self.num_chunks, B * H * W // self.num_chunks)
+                mean_max = y.max(-1)[0].mean(-1)
+                mean_min = y.min(-1)[0].mean(-1)
+                mean = y.view(C, -1).mean(-1)
+                n = y.size(-1)
+            else:
+                # calibration: the chunked reductions in one device pass (qnn_rangebn_stats_f32)
+                mean_max, mean_min, mean, n = rangebn_stats(x, self.num_chunks)
             scale_fix = (0.5 * 0.35) * (1 + (math.pi * math.log(4)) ** 0.5) / ((2 * math.log(n)) ** 0.5)
             scale = 1 / ((mean_max - mean_min) * scale_fix + self.eps)
             self.running_mean.detach().mul_(self.momentum).add_(mean * (1 - self.momentum))
@@ -717,9 +886,17 @@ class RangeBN(nn.Module):
             scale = self.running_var
         with torch.no_grad():
             sq, wq, bq = self._params(scale.detach().contiguous()) if x.is_cuda else _cpu_unsupported("RangeBN")
+        if grad:  # the quantizers of :486-498 are straight-through (:105-109)
+            sq = _Passthrough.apply(scale, sq)
+            if self.weight is not None:
+                wq = _Passthrough.apply(self.weight, wq)
+            if self.bias is not None:
+                bq = _Passthrough.apply(self.bias, bq)
         out = (x - mean.view(1, mean.size(0), 1, 1)) * sq.view(1, sq.size(0), 1, 1)
         out = out * wq.view(1, wq.size(0), 1, 1)
         out = out + bq.view(1, bq.size(0), 1, 1)
+        if grad and self.num_bits_grad is not None:
+            out = quantize_grad(out, num_bits=self.num_bits_grad)  # :500-501
         if out.size(3) == 1 and out.size(2) == 1:
             out = out.squeeze(-1).squeeze(-1)
         return out

@@ -193,6 +193,49 @@ def gen_model(Q, RQ, MQ, name, fac, kw, shape, calib_b):
     print(f"model_{name}: logits{tuple(logits.shape)} argmax={logits.argmax(1).tolist()}")
 
 
+# training-side fixtures: (name, kind, kwargs, input shape, num_bits_grad, biprecision)
+TRAIN = [
+    ("train_c3x3_biprec", "conv", dict(in_channels=16, out_channels=32, kernel_size=3, stride=1, padding=1, bias=True),
+     (2, 16, 8, 8), 8, True),
+    ("train_c3x3_gradq", "conv", dict(in_channels=16, out_channels=32, kernel_size=3, stride=2, padding=1, bias=True),
+     (2, 16, 9, 9), 8, False),
+    ("train_c3x3_plain", "conv", dict(in_channels=16, out_channels=16, kernel_size=3, stride=1, padding=1, bias=False),
+     (2, 16, 8, 8), None, False),
+    ("train_fc_biprec", "linear", dict(in_features=64, out_features=10, bias=True), (4, 64), 8, True),
+]
+
+
+def gen_train(Q, name, kind, kw, shape, nbg, biprec):
+    """One reference QConv2d / QLinear in training mode: forward on a fresh batch (QuantMeasure
+    batch statistics), backward of a fixed output gradient.  The stochastic rounding draw of the
+    gradient quantizer is torch's first CPU draw after manual_seed(NOISE_SEED); it is stored too,
+    so a device run can be fed the same noise."""
+    torch.manual_seed(0)
+    args = dict(num_bits=8, num_bits_weight=8, num_bits_grad=nbg, biprecision=biprec)
+    mod = Q.QConv2d(**kw, **args) if kind == "conv" else Q.QLinear(**kw, **args)
+    wrap = nn.Sequential(mod)
+    synthetic.init_params(wrap, seed=9)
+    wrap.train()
+    x = synthetic.input_batch(shape, 500).requires_grad_(True)
+    y = wrap(x)
+    gy = synthetic.input_batch(tuple(y.shape), 501)
+    NOISE_SEED = 1234
+    torch.manual_seed(NOISE_SEED)
+    noise = torch.empty(tuple(y.shape)).uniform_(-0.5, 0.5)
+    torch.manual_seed(NOISE_SEED)  # the reference's backward draws exactly this
+    y.backward(gy)
+    rec = {"config": np.array(json.dumps(dict(kind=kind, kw=kw, shape=shape, num_bits_grad=nbg, biprecision=biprec,
+                                                param_seed=9, x_seed=500, gy_seed=501, noise_seed=NOISE_SEED))),
+           "x": x.detach().numpy(), "y": y.detach().numpy(), "gy": gy.numpy(), "noise": noise.numpy(),
+           "grad_x": x.grad.numpy(), "grad_w": mod.weight.grad.numpy(),
+           "param_checksum": np.array(synthetic.param_checksum(wrap))}
+    if mod.bias is not None:
+        rec["grad_b"] = mod.bias.grad.numpy()
+    rec.update(buffers(wrap))
+    savez(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(f"{name}: y{tuple(y.shape)} |grad_x|={x.grad.abs().sum():.6g} |grad_w|={mod.weight.grad.abs().sum():.6g}")
+
+
 def main():
     global OUT
     ap = argparse.ArgumentParser()
@@ -212,6 +255,9 @@ def main():
     for M in MODELS:
         if not want or M[0] in want:
             gen_model(Q, RQ, MQ, *M)
+    for T in TRAIN:
+        if not want or T[0] in want:
+            gen_train(Q, *T)
 
 
 if __name__ == "__main__":
