@@ -70,7 +70,7 @@ class _Passthrough(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, q):
-        return q.view_as(q)
+        return q.clone()  # a fresh tensor: a view of an input could not be modified in place downstream
 
     @staticmethod
     def backward(ctx, g):
@@ -168,7 +168,10 @@ class _QuantizeGrad(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, num_bits, min_value, max_value, stochastic):
         ctx.args = (num_bits, min_value, max_value, stochastic)
-        return x.view_as(x)
+        # the reference returns its input (quantize.py:121); a copy here, because the models
+        # apply nn.ReLU(inplace=True) to this output and autograd forbids in-place writes to a
+        # view returned by a custom Function
+        return x.clone()
 
     @staticmethod
     def backward(ctx, grad_output):

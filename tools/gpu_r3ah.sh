@@ -13,4 +13,5 @@ tail -1 gpurun_out/r3ah_smoke.log
 timeout -k 10 300 python -u bench.py > gpurun_out/r3ah_bench.json 2> gpurun_out/r3ah_bench.err || exit $?
 cut -c1-200 gpurun_out/r3ah_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 20 --no-cpu-baseline --module-path 0 > gpurun_out/r3ah_bench_rocprof.log 2>&1 || exit $?
-bash tools/gpu_r3af.sh
+timeout -k 10 300 python -u bench_layers.py --only headline r50_l4 > gpurun_out/r3ah_headline.jsonl 2>> gpurun_out/r3ah_bench.err || exit $?
+cut -c1-300 gpurun_out/r3ah_headline.jsonl
