@@ -39,9 +39,11 @@ LAYERS = {
 }
 
 
-def run(name, cfg, reps, dev):
+def run(name, cfg, reps, dev, tile=None):
     cin, cout, k, st, pd, N, H = cfg
     m = QConv2d(cin, cout, k, stride=st, padding=pd, bias=False, num_bits_grad=8, biprecision=True)
+    if tile is not None:
+        m.qnn_tile = tile + 1  # force tile configuration `tile` (qnn_conv_desc.tile)
     wrap = nn.Sequential(m)
     synthetic.init_params(wrap, 1)
     m.quantize_input.running_min.fill_(0.0)
@@ -83,13 +85,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", nargs="*")
+    ap.add_argument("--tiles", nargs="*", type=int, help="force each of these tile configurations in turn")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     _lib.load()
     for name, cfg in LAYERS.items():
         if a.only and not any(o in name for o in a.only):
             continue
-        print(json.dumps(run(name, cfg, a.reps, dev)), flush=True)
+        for t in (a.tiles or [None]):
+            print(json.dumps(run(name, cfg, a.reps, dev, t)), flush=True)
 
 
 if __name__ == "__main__":
