@@ -28,6 +28,7 @@ steady-state eval forward issues no synchronisation.
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -448,6 +449,11 @@ def s2d_kmask(kh, kw, cin_g, kpad, dev):
     return torch.from_numpy(m).to(dev)
 
 
+# The drop-in module path times every tile configuration of a layer the first time it sees an
+# input shape and keeps the fastest (MODULE_AUTOTUNE[0] = False: the library's cost model).
+MODULE_AUTOTUNE = [os.environ.get("QNN_MODULE_AUTOTUNE", "1") != "0"]
+
+
 class _QLayerMixin:
     """Shared int8 machinery of QConv2d / QLinear (QuantNode subclasses)."""
 
@@ -546,6 +552,33 @@ class _QLayerMixin:
         self._qpack = pk
         return pk
 
+    def _tuned_tile(self, xq, pk, d, e, st, key, reps=3):
+        """The fastest tile configuration for this layer at this input shape, timed once on the
+        device (HIP events on the launch stream) the first time the shape is seen, as the
+        engine's autotune does; every configuration computes the identical output, so this
+        only changes speed.  0 (the cost model) while a hipGraph is being captured."""
+        tuned = self.__dict__.setdefault("_tuned", {})
+        if key in tuned:
+            return tuned[key]
+        best = None
+        for k in range(_lib.CONV_TILES):
+            d.tile = k + 1
+            try:
+                _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
+            except _lib.QnnError:
+                continue  # configuration not built for this layer
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            if best is None or ms < best[1]:
+                best = (k, ms)
+        tuned[key] = 0 if best is None else best[0] + 1
+        return tuned[key]
+
     @staticmethod
     def _geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, dev):
         gk = (H, W)
@@ -632,6 +665,8 @@ class _QLayerMixin:
         e.nwc, e.nclass = g[5], g[2] * g[5]
         e.bias = None if pk.qbias is None else pk.qbias.data_ptr()
         e.out_f32 = y.data_ptr()
+        if self.qnn_tile == 0 and MODULE_AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
+            d.tile = self._tuned_tile(xq, pk, d, e, st, (N, H, W, Ho, Wo))
         _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
         self._last_conv = (d, e)  # launch descriptors, for profiling tools (qnn_conv_plan)
         self._last_xq = xq if self.qnn_keep_input else None  # the codes, for tools that re-issue the launch

@@ -11,6 +11,11 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 for p in (REPO, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
+# The module path's per-shape autotune (qnn.quantize.MODULE_AUTOTUNE) would time every tile
+# configuration for each of the many fresh layers the tests build; the tests force or use the
+# cost model's configuration instead (every configuration is checked on its own), and
+# tests/test_gpu_tiles.py::test_module_autotune_bitwise covers the autotune itself.
+os.environ.setdefault("QNN_MODULE_AUTOTUNE", "0")
 
 
 def pytest_configure(config):

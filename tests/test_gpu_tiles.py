@@ -177,3 +177,31 @@ def test_engine_bench_batch_bitwise_vs_module_path(gpu, fixture, batch):
     eng(xg)
     print(f"{fixture} b{batch} autotuned tiles: {[k for k, _ in eng.tiles]}")
     assert torch.equal(eng.head_input, feat.permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("name", ["headline_3x3_256_14", "r18_3x3_64_56"])
+def test_module_autotune_bitwise(gpu, name):
+    """The drop-in module path's per-shape autotune picks a configuration built for the layer,
+    remembers it per input shape, and changes nothing but speed: bitwise the cost model's
+    output."""
+    from qnn import quantize as Q
+    wrap, x, ref = _case(name)
+    wrap = wrap.to(gpu)
+    m = wrap[0]
+    xg = x.to(gpu)
+    with torch.no_grad():
+        y0 = wrap(xg)
+    Q.MODULE_AUTOTUNE[0] = True
+    try:
+        with torch.no_grad():
+            y1 = wrap(xg)
+            y2 = wrap(xg)
+    finally:
+        Q.MODULE_AUTOTUNE[0] = False
+    assert len(m._tuned) == 1
+    k = next(iter(m._tuned.values()))
+    assert 1 <= k <= _lib.CONV_TILES
+    from qnn.engine import Engine
+    assert Engine.plan(*m._last_conv)[0] == k - 1
+    assert torch.equal(y0, y1) and torch.equal(y1, y2)
+    _close(y1, ref)
