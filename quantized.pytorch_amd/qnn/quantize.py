@@ -449,9 +449,10 @@ def s2d_kmask(kh, kw, cin_g, kpad, dev):
     return torch.from_numpy(m).to(dev)
 
 
-# The drop-in module path times every tile configuration of a layer the first time it sees an
-# input shape and keeps the fastest (MODULE_AUTOTUNE[0] = False: the library's cost model).
-MODULE_AUTOTUNE = [os.environ.get("QNN_MODULE_AUTOTUNE", "1") != "0"]
+# QNN_MODULE_AUTOTUNE=1 (or MODULE_AUTOTUNE[0] = True): the drop-in module path times every tile
+# configuration of a layer the first time it sees an input shape and keeps the fastest; off, it
+# launches the library's cost-model choice.
+MODULE_AUTOTUNE = [os.environ.get("QNN_MODULE_AUTOTUNE", "0") == "1"]
 
 
 class _QLayerMixin:
