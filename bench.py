@@ -27,7 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec, 8-bit ResNet-18 224×224 @1/2/4/8 GPU; % int8-MFMA roofline"
-ROUND = 3  # profiles/rNN_traffic_* from an earlier round measured other kernels: never cited as traffic
+ROUND = 4  # profiles/rNN_traffic_* from an earlier round measured other kernels: never cited as traffic
 PEAK_INT8_TOPS = 5000.0   # dense int8 MFMA, 256 CU x 2.4 GHz (MI355X_MICROARCH.md: 2x bf16 2.5 PF)
 PEAK_HBM_GBS = 8000.0
 
@@ -185,6 +185,42 @@ def throughput(global_batch, steps, elapsed):
     return global_batch * steps / elapsed
 
 
+CONV_LAUNCHES = ("qnn_qconv2d_fwd", "qnn_qconv2d_maxpool_fwd")
+
+
+def in_graph_times(engine, reps):
+    """In-graph kernel time per forward of each launch kind, measured live with HIP events:
+    the launches of one kind (every contraction, or every depthwise conv, ...) are captured in
+    plan order as a hipGraph of their own, which is replayed `reps` times between two events
+    recorded on torch's current stream (the stream the replay runs on).  Each launch thus runs
+    once per replay in the same order, on the same buffers and with the same cache history
+    per forward as inside the full graph -- no back-to-back repeats of one launch over warm
+    operands -- and the figure includes the in-graph launch boundaries (~1 us each), so it
+    bounds the kernels' own rate from below.  Returns ({kind: ms per forward}, conv ms)."""
+    out = {}
+    for name in dict.fromkeys(engine.launch_names):
+        g, _n = engine.capture_subset([name])
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        e1.synchronize()
+        out[name] = e0.elapsed_time(e1) / reps
+        del g
+    conv_names = [n for n in CONV_LAUNCHES if n in out]
+    g, _n = engine.capture_subset(conv_names)
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    e1.synchronize()
+    return out, e0.elapsed_time(e1) / reps
+
+
 def model_name(arch, depth):
     return "mobilenet" if arch == "mobilenet" else f"resnet{depth}"
 
@@ -256,26 +292,7 @@ def main():
 
     elapsed = timed_run(step, args.steps, args.warmup, world, torch.cuda.synchronize)
 
-    # Per-launch HIP-event timing of every kernel of one forward: each launch of the list the
-    # graph replays runs `reps` times back to back between two events on the launch stream
-    # (torch's current stream, which every qnn call is issued on), so the per-call host
-    # dispatch gap is amortised as in the replay and the figure is the kernel's own duration
-    # (the rocprofv3 kernel trace of the same launches agrees: profiles/r3_layers_*.json)
-    reps = 10
-    per_kernel = {}
-    st = _lib.stream_of(engine.input)
-    with torch.no_grad():
-        engine._run_ops()
-        for op, name in zip(engine.ops, engine.launch_names):
-            op(st)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
-                op(st)
-            e1.record()
-            e1.synchronize()
-            per_kernel[name] = per_kernel.get(name, 0.0) + e0.elapsed_time(e1) / reps
-    conv_ms_per_fwd = per_kernel.get("qnn_qconv2d_fwd", 0.0) + per_kernel.get("qnn_qconv2d_maxpool_fwd", 0.0)
+    per_kernel, conv_ms_per_fwd = in_graph_times(engine, reps=max(10, args.steps))
     launches = engine.num_launches
 
     module_ips = None
@@ -326,7 +343,9 @@ def main():
                          "kernel_ms_per_forward": round(conv_ms_per_fwd, 4),
                          "model_frac": round(total_ops / (ms_per_step * 1e-3) / 1e12 / PEAK_INT8_TOPS, 4)},
             "engine": {"launches_per_forward": launches, "hipgraph": True,
-                       "kernel_ms_per_forward": {k: round(v, 4) for k, v in per_kernel.items()}},
+                       "kernel_ms_per_forward": {k: round(v, 4) for k, v in per_kernel.items()},
+                       "kernel_ms_source": "in-graph: each launch kind captured as its own hipGraph in plan order, "
+                                           "replayed between HIP events (bench.in_graph_times)"},
             "module_path_images_per_s": None if module_ips is None else round(module_ips, 1),
             "cpu_baseline": None,
         }

@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 7
+#define QNN_ABI_VERSION 8
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -384,6 +384,13 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
                      const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min, float x_scale,
                      const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
                      const qnn_code_out* code0, qnn_stream_t stream);
+
+/* The same operation always on the generic depthwise kernel (any kh x kw, stride, channel
+ * count): the bitwise reference the tests hold qnn_dwconv_fused's 3x3 fast kernel to. */
+int qnn_dwconv_fused_generic(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                             const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
+                             float x_scale, const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
+                             const qnn_code_out* code0, qnn_stream_t stream);
 
 /* nn.AvgPool2d(k) over the whole k x k map (resnet_quantized.py:153, mobilenet_quantized.py:157)
  * on fp32 x [n*hw][c] (NHWC, or the C-tile layout when x_tiled): mean = (sum in row-major

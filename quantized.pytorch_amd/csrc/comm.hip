@@ -1,7 +1,7 @@
 // RCCL logits gather behind the C ABI: the one collective of the
 // data-parallel eval forward -- each rank's [B/W, classes] fp32 logits to rank 0 over xGMI --
 // replacing nn.DataParallel's gather (reference main.py:345).  One process per GPU; the
-// communicator is the library's only global mutable state (guarded for init / destroy).
+// communicator is the library's only global mutable state (every entry point holds its mutex).
 #include <string.h>
 
 #include <mutex>
@@ -58,6 +58,8 @@ extern "C" int qnn_comm_destroy(void) {
 }
 
 extern "C" int qnn_gather_f32(const float* send, float* recv, size_t count, int root, qnn_stream_t stream) {
+  // held across the enqueue: a concurrent qnn_comm_destroy cannot free the communicator under it
+  std::lock_guard<std::mutex> lock(g_comm_mu);
   QNN_REQUIRE(g_comm, "no communicator (qnn_comm_init)");
   QNN_REQUIRE(root >= 0 && root < g_world, "root out of range");
   if (count == 0) return QNN_OK;

@@ -478,10 +478,14 @@ int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stri
   return QNN_OK;
 }
 
-int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
-                     const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min, float x_scale,
-                     const float* bias, const qnn_bn_params* bn, int relu, float* out_f32, const qnn_code_out* code0,
-                     qnn_stream_t stream) {
+}  // extern "C"
+
+// The depthwise dispatcher: the 3x3 register-pipelined kernel where the shapes allow it, else
+// (or when `generic`, the bitwise reference the tests compare it with) the generic kernel.
+static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                        const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
+                        float x_scale, const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
+                        const qnn_code_out* code0, qnn_stream_t stream, bool generic) {
   QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && cp >= c && cp % 4 == 0 && kh > 0 && kw > 0 &&
                   sh > 0 && sw > 0 && pad >= 0,
               "bad shape");
@@ -497,10 +501,8 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
   memset(&b, 0, sizeof(b));
   if (bn) b = *bn;
   const qnn_code_out c0 = code0 ? *code0 : none_code();
-  const char* fg = getenv("QNN_DW_GENERIC");  // read per call: tests compare both kernels bitwise
-  const int force_generic = fg ? atoi(fg) : 0;
   constexpr int CPT = 2 * QNN_DW_P;
-  const bool fast = !force_generic && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) && c % CPT == 0 &&
+  const bool fast = !generic && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) && c % CPT == 0 &&
                     c / CPT <= 256 && cp % 8 == 0 && (((uintptr_t)x) & 7) == 0 && (((uintptr_t)w_hat_t) & 15) == 0 &&
                     (!out_f32 || (((uintptr_t)out_f32) & 15) == 0) &&
                     (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0));
@@ -511,8 +513,7 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
     QNN_REQUIRE(groups < (1LL << 31) && (int64_t)n * hp * wp * cp < (1LL << 40), "depthwise too large");
     auto kern = sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P> : dwconv3_kernel<2, 2, QNN_DW_P>;
     // grid-stride, sized to the resident capacity (the loop is software-pipelined)
-    static int num_cu = 0;
-    if (!num_cu && hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) num_cu = 256;
+    const int num_cu = device_cu_count();
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     const int blocks = (int)std::min<int64_t>(cdiv(groups, 256 / ct), (int64_t)num_cu * per_cu);
@@ -527,6 +528,24 @@ int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int 
                      x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0);
   QNN_LAUNCH_CHECK("qnn_dwconv_fused");
   return QNN_OK;
+}
+
+extern "C" {
+
+int qnn_dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                     const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min, float x_scale,
+                     const float* bias, const qnn_bn_params* bn, int relu, float* out_f32, const qnn_code_out* code0,
+                     qnn_stream_t stream) {
+  return dwconv_fused(x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min, x_scale, bias, bn, relu,
+                      out_f32, code0, stream, false);
+}
+
+int qnn_dwconv_fused_generic(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                             const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
+                             float x_scale, const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
+                             const qnn_code_out* code0, qnn_stream_t stream) {
+  return dwconv_fused(x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min, x_scale, bias, bn, relu,
+                      out_f32, code0, stream, true);
 }
 
 int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,

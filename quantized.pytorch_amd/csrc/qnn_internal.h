@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <string>
 
 #include "../../include/qnn.h"
@@ -22,6 +23,19 @@ int arg_error(const char* what);
   do {                         \
     if (!(cond)) return ::qnn::arg_error(msg); \
   } while (0)
+
+// CU count of the calling thread's current device, queried once per device (race-free: a
+// concurrent first call queries twice and stores the same value)
+inline int device_cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
 
 #define QNN_LAUNCH_CHECK(what) \
   do {                         \

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (binds the process HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 CONV_TILES = 40  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
@@ -35,6 +35,7 @@ class ResLink(ctypes.Structure):
 
 
 MAX_RES = 4  # QNN_MAX_RES
+COMM_ID_BYTES = 128  # QNN_COMM_ID_BYTES
 
 
 class Epilogue(ctypes.Structure):
@@ -88,6 +89,8 @@ SIGNATURES = {
     "qnn_maxpool_bn": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _PB, c_int, c_ptr,
                        c_int, c_ptr, c_ptr, _PC, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
+                         c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
+    "qnn_dwconv_fused_generic": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],

@@ -107,7 +107,9 @@ def load_maybe_calibrate(model, checkpoint, save_dir, model_name, depth, calib_b
                     model(x.to(next(model.parameters()).device))
             set_measure_mode(model, False)
             from . import dist as qdist
-            qdist.allreduce_calibration(model)
+            # weighted by this rank's samples per calibration batch (ragged shards merge exactly)
+            nb = len(calib_batches)
+            qdist.allreduce_calibration(model, samples=sum(int(x.shape[0]) for x in calib_batches) / nb if nb else 0)
             if not torch.distributed.is_initialized() or torch.distributed.get_rank() == 0:
                 save_checkpoint(mpath, model, model_name=model_name, config=str({"depth": depth}))
             how = "calibrated"

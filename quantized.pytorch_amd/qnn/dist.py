@@ -65,12 +65,13 @@ def allreduce_calibration(model, group=None, samples=1):
     per calibration batch: its shard size), flattened into one fp32 bucket and all-reduced
     once (RCCL on GPU tensors, gloo on CPU).  Call after every rank ran the same number
     of measure-mode batches.  Exact for the extrema means and the means; the std and the
-    RangeBN scale merge as weighted means (module docstring).  No-op for world size 1."""
+    RangeBN scale merge as weighted means (module docstring).  No-op for world size 1.
+    A rank with samples == 0 takes part with weight 0 (its buffers are ignored); invalid
+    weights (negative, or every rank 0) raise ValueError on EVERY rank, after the one
+    collective, so no rank is left waiting in it."""
     from .quantize import QuantMeasure, RangeBN
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
-    if samples <= 0:
-        raise ValueError("allreduce_calibration: samples must be > 0")
     bufs = []
     for m in model.modules():
         if isinstance(m, QuantMeasure):
@@ -79,10 +80,15 @@ def allreduce_calibration(model, group=None, samples=1):
             bufs += [m.running_mean, m.running_var]
     if not bufs:
         return
-    flat = torch.cat([b.detach().reshape(-1).to(torch.float64) for b in bufs] +
-                     [torch.ones(1, dtype=torch.float64, device=bufs[0].device)]) * float(samples)
+    w = float(samples) if samples > 0 else 0.0
+    dev = bufs[0].device
+    vals = torch.cat([b.detach().reshape(-1).to(torch.float64) for b in bufs])
+    vals = vals * w if w > 0 else torch.zeros_like(vals)  # weight 0: never 0 * inf = nan
+    flat = torch.cat([vals, torch.tensor([w, 1.0 if samples < 0 else 0.0], dtype=torch.float64, device=dev)])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-    flat = flat[:-1] / flat[-1]
+    if flat[-1].item() > 0 or flat[-2].item() <= 0:
+        raise ValueError("allreduce_calibration: samples must be >= 0 on every rank and > 0 on at least one")
+    flat = flat[:-2] / flat[-2]
     off = 0
     with torch.no_grad():
         for b in bufs:
@@ -190,7 +196,7 @@ class AbiComm:
         import ctypes
         from . import _lib
         self.rank, self.world = rank, world
-        uid = (ctypes.c_ubyte * 128)()
+        uid = (ctypes.c_ubyte * _lib.COMM_ID_BYTES)()
         if rank == 0:
             _lib.call("qnn_comm_unique_id", ctypes.byref(uid), ctypes.sizeof(uid))
         if world > 1:
@@ -198,7 +204,7 @@ class AbiComm:
             if dist.get_backend() == "nccl":
                 t = t.cuda()
             dist.broadcast(t, 0)
-            uid = (ctypes.c_ubyte * 128)(*t.cpu().tolist())
+            uid = (ctypes.c_ubyte * _lib.COMM_ID_BYTES)(*t.cpu().tolist())
         _lib.call("qnn_comm_init", rank, world, ctypes.byref(uid))
 
     def gather(self, send, recv=None, root=0):

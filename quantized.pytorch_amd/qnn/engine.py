@@ -646,6 +646,24 @@ class Engine:
             self._run_ops()
         torch.cuda.synchronize(self.dev)
 
+    def capture_subset(self, names):
+        """A hipGraph of only the launches whose ABI name is in `names`, in plan order (for
+        in-graph timing of one kernel kind: bench.py's roofline).  The buffers are the engine's
+        own, so replaying it recomputes those launches' outputs from the current inputs."""
+        idx = [i for i, n in enumerate(self.launch_names) if n in set(names)]
+        if not idx:
+            raise ValueError(f"qnn.Engine: no launch named {sorted(set(names))}")
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(g, stream=s):
+            st = _lib.stream_of(self.input)
+            for i in idx:
+                self.ops[i](st)
+        torch.cuda.synchronize(self.dev)
+        return g, len(idx)
+
     def __call__(self, x=None):
         """Run one forward.  Returns the engine's static logits buffer [batch, classes]: the
         next call overwrites it (clone() to keep a result)."""

@@ -18,8 +18,10 @@ Execution model:
   linear (`F.conv2d`/`F.linear`, quantize.py:350-352, :429-430) and the
   QuantMeasure / RangeBN statistics updates (:225-239, :466-482) in torch ops.
   This is calibration, off the hot path.
-* forward only: no autograd through the int8 path (training is out of scope,
-  SURVEY.md §2 row 1).
+* training: with autograd on, the same int8 forward runs inside
+  `_QLayerTrain`, whose backward restates the reference's graph -- straight-through
+  quantizers (quantize.py:105-109), UniformQuantizeGrad on the output gradient
+  (:112-139, `qnn_grad_quant_f32`) and the biprecision split (:142-156).
 
 Host-scalar caching: the reference reads `float(running_min)` on every call
 (2 device->host syncs per layer, quantize.py:249).  Here ranges, packed weights

@@ -51,7 +51,17 @@ def test_bindings_cover_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.qnn_abi_version() == 7
+    from qnn import _lib
+    assert lib.qnn_abi_version() == _lib.ABI_VERSION == 8
+
+
+def test_header_constants_match_bindings():
+    from qnn import _lib
+    src = open(HEADER).read()
+    defs = dict(re.findall(r"^#define\s+(QNN_\w+)\s+(\d+)", src, flags=re.M))
+    assert int(defs["QNN_ABI_VERSION"]) == _lib.ABI_VERSION
+    assert int(defs["QNN_MAX_RES"]) == _lib.MAX_RES
+    assert int(defs["QNN_COMM_ID_BYTES"]) == _lib.COMM_ID_BYTES
 
 
 def test_argument_validation_without_device(lib):

@@ -239,3 +239,40 @@ def test_allreduce_calibration_ragged_shards_weighted():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert sorted(q.get(timeout=10) for _ in range(2)) == [(0, True), (1, True)]
+
+
+def _calib_weights_worker(rank, world, port, weights, q):
+    from qnn.dist import allreduce_calibration
+    from qnn.quantize import QuantMeasure
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    qmod = QuantMeasure(8)
+    with torch.no_grad():
+        qmod.running_min.fill_(float("-inf") if weights[rank] == 0 else -1.0 - rank)
+        qmod.running_max.fill_(2.0 + rank)
+    try:
+        allreduce_calibration(qmod, samples=weights[rank])
+        q.put((rank, "ok", float(qmod.running_min), float(qmod.running_max)))
+    except ValueError:
+        q.put((rank, "ValueError", None, None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("weights,expect", [
+    ((0, 4), ("ok", -2.0, 3.0)),            # a rank with no calibration samples takes part with weight 0
+    ((-1, 4), ("ValueError", None, None)),  # an invalid weight raises on EVERY rank (no rank hangs)
+    ((0, 0), ("ValueError", None, None)),
+])
+def test_allreduce_calibration_weights_collective(weights, expect):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calib_weights_worker, args=(r, 2, port, weights, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert [r[1:] for r in res] == [expect, expect]

@@ -11,7 +11,6 @@ against an fp64 restatement of the reference's depthwise conv (quantize.py:343,
 groups == cin) on the dequantized codes.
 """
 import ctypes
-import os
 
 import numpy as np
 import pytest
@@ -24,13 +23,9 @@ pytestmark = pytest.mark.gpu
 
 def _run(xcodes, geom, wt, bias, bn, relu, out_f32, code, generic, st):
     n, h, w, pad, hp, wp, cp, c, k, s, ho, wo, xmin, xs = geom
-    os.environ["QNN_DW_GENERIC"] = "1" if generic else "0"
-    try:
-        _lib.call("qnn_dwconv_fused", _lib.ptr(xcodes), n, h, w, pad, hp, wp, cp, c, _lib.ptr(wt), k, k, s, s, ho, wo,
-                  xmin, xs, None if bias is None else _lib.ptr(bias), None if bn is None else ctypes.byref(bn), relu,
-                  _lib.ptr(out_f32), ctypes.byref(code), st)
-    finally:
-        os.environ.pop("QNN_DW_GENERIC", None)
+    _lib.call("qnn_dwconv_fused_generic" if generic else "qnn_dwconv_fused", _lib.ptr(xcodes), n, h, w, pad, hp, wp,
+              cp, c, _lib.ptr(wt), k, k, s, s, ho, wo, xmin, xs, None if bias is None else _lib.ptr(bias),
+              None if bn is None else ctypes.byref(bn), relu, _lib.ptr(out_f32), ctypes.byref(code), st)
     torch.cuda.synchronize()
 
 
