@@ -85,6 +85,8 @@ def allreduce_calibration(model, group=None, samples=1):
     vals = torch.cat([b.detach().reshape(-1).to(torch.float64) for b in bufs])
     vals = vals * w if w > 0 else torch.zeros_like(vals)  # weight 0: never 0 * inf = nan
     flat = torch.cat([vals, torch.tensor([w, 1.0 if samples < 0 else 0.0], dtype=torch.float64, device=dev)])
+    if dist.get_backend(group) == "gloo":
+        flat = flat.cpu()  # gloo is the host transport (device buffers are staged through it)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     if flat[-1].item() > 0 or flat[-2].item() <= 0:
         raise ValueError("allreduce_calibration: samples must be >= 0 on every rank and > 0 on at least one")
@@ -155,8 +157,11 @@ class ShardedInference:
             slots = self._slots[shape] = [None, None]
         k = self._k % 2
         self._k += 1
+        # gloo is the host transport: device outputs are staged through host slots (RCCL moves
+        # device buffers directly over xGMI)
+        host = self.world > 1 and y_local.is_cuda and dist.get_backend(self.group) == "gloo"
         if slots[k] is None:
-            send = y_local.new_zeros(shape)
+            send = torch.zeros(shape, dtype=y_local.dtype) if host else y_local.new_zeros(shape)
             recv = [torch.empty_like(send) for _ in range(self.world)] if self.rank == self.root else None
             slots[k] = [send, recv, None]
         send, recv, prev = slots[k]
@@ -168,7 +173,8 @@ class ShardedInference:
             return pend
         work = dist.gather(send, recv, dst=self.root, group=self.group, async_op=True)
         if self.rank == self.root:
-            fn = lambda: torch.cat([b[: e_ - s_] for b, (s_, e_) in zip(recv, self.bounds)])
+            dev = y_local.device
+            fn = lambda: torch.cat([b[: e_ - s_] for b, (s_, e_) in zip(recv, self.bounds)]).to(dev)
         else:
             fn = lambda: None
         slots[k][2] = pend = _Pending(work, fn)

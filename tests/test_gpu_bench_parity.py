@@ -129,6 +129,43 @@ def test_resident_band_natural_occupancy(gpu, name):
         assert two, f"no resident-band configuration runs two co-resident blocks per CU on a full grid: {ran}"
 
 
+RBP_SHAPES = [  # (name, cin, cout, k, stride, pad, N, H): the two-team kernel's target layers
+    ("headline_3x3_256_14_b256", 256, 256, 3, 1, 1, 256, 14),
+    ("k4608_3x3_512_7_b256", 512, 512, 3, 1, 1, 256, 7),
+    ("r18_3x3_256_14_b128", 256, 256, 3, 1, 1, 128, 14),
+    ("ragged_3x3_256_14_b37", 256, 256, 3, 1, 1, 37, 14),
+]
+
+
+@pytest.mark.parametrize("name", [s[0] for s in RBP_SHAPES])
+def test_two_team_resident_band_bench(gpu, name):
+    """qconv_rbp_kernel (two priority teams, chunked band, LDS counters instead of barriers) on
+    full grids: bitwise against the ring kernel, twice (run-to-run identical), and the ring
+    kernel against the oracle on the first and last images."""
+    _, cin, cout, k, st, pd, N, H = next(s for s in RBP_SHAPES if s[0] == name)
+    wrap, x = _layer(cin, cout, k, st, pd, N, H, 43)
+    wrap = wrap.to(gpu)
+    xg = x.to(gpu)
+    y_ring, d, e = _run(wrap, xg, RING)
+    idx = torch.tensor([0, N - 1])
+    _close(y_ring[idx], _oracle_rows(wrap.cpu(), x, idx))
+    wrap = wrap.to(gpu)
+    from qnn.engine import Engine
+    ran = []
+    for t in _lib.tile_ids("qconv_rbp_kernel"):
+        d.tile = t + 1
+        if not Engine._plan_ok(d, e):
+            continue
+        for rep in range(2):
+            y, _, _ = _run(wrap, xg, t)
+            torch.cuda.synchronize()
+            ndiff = int((y != y_ring).sum())
+            assert ndiff == 0, f"config {t} run {rep}: {ndiff} outputs != config {RING}"
+        ran.append((t, Engine.plan(d, e)[3]))
+    print(f"{name}: two-team configurations (id, grid) = {ran}")
+    assert ran, "no two-team configuration is built for this shape"
+
+
 DIRECT_SHAPES = [  # (name, direct-fragment configuration index, cin, cout, k, stride, pad, N, H)
     ("mbn_stem_s2d_3x3_32_b256", 0, 3, 32, 3, 2, 1, 256, 224),
     ("r_stem_s2d_7x7_64_b128", 1, 3, 64, 7, 2, 3, 128, 224),

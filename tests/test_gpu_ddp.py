@@ -1,0 +1,206 @@
+"""Multi-rank paths with device tensors, at world size 2 on the one GPU of a box: both ranks
+are freshly spawned processes on cuda:0 joined by the gloo backend (RCCL refuses two ranks on
+one device; the 8-GPU RCCL path is the same code with backend "nccl").
+
+* §8(f4) training under DistributedDataParallel (reference qdistiler_main.py:882-891): each
+  rank runs the quantized model's training step (int8 forward, straight-through quantizers,
+  8-bit stochastic gradient quantization) on its shard inside DDP; the averaged gradients must
+  equal the mean of the single-process gradients of the two shards (same stochastic draws).
+* the data-parallel eval path (reference main.py:344-345, nn.DataParallel): each rank
+  calibrates on its own shard, allreduce_calibration merges the statistics (sample-weighted),
+  a qnn.Engine runs the rank's shard and ShardedInference gathers the logits on rank 0; they
+  must equal, bitwise, one engine over the whole batch built from the same merged statistics.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FIXTURE = "model_resnet18_cifar"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(target, args, world=2, timeout=240):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=timeout)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, f"rank exit codes {codes}"
+
+
+def _init(rank, world, port):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "quantized.pytorch_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from qnn import _lib
+    _lib.load()
+    return dist
+
+
+# ---------------------------------------------------------------- DDP training step
+GB_TRAIN = 8
+
+
+def _train_batch(dev):
+    from qnn import synthetic
+    x = synthetic.input_batch((GB_TRAIN, 3, 32, 32), 77).to(dev)
+    y = (torch.arange(GB_TRAIN, device=dev) * 3) % 10
+    return x, y
+
+
+def _shard_grads(model, x, y, seed):
+    """One training step's gradients of `model` on (x, y), the stochastic draws from `seed`."""
+    import torch.nn.functional as F
+    torch.manual_seed(seed)
+    model.zero_grad(set_to_none=True)
+    F.cross_entropy(model(x), y).backward()
+
+
+def _ddp_worker(rank, world, port, out):
+    dist = _init(rank, world, port)
+    from conftest import load_fixture
+    from fixtures_util import build_model
+    from qnn.dist import shard_bounds
+    dev = torch.device("cuda:0")
+    model, _ = build_model(load_fixture(FIXTURE))
+    model = model.to(dev).train()
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], output_device=0)
+    x, y = _train_batch(dev)
+    s, e = shard_bounds(GB_TRAIN, world, rank)
+    _shard_grads(ddp, x[s:e], y[s:e], 100 + rank)
+    if rank == 0:
+        torch.save({n: p.grad.detach().cpu() for n, p in model.named_parameters()}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_training_step_world2(gpu, tmp_path):
+    from conftest import load_fixture
+    from fixtures_util import build_model
+    from qnn.dist import shard_bounds
+    out = str(tmp_path / "ddp_grads.pt")
+    _spawn(_ddp_worker, (out,))
+    ddp = torch.load(out, weights_only=True)
+    x, y = _train_batch(gpu)
+    per = []
+    for r in range(2):
+        model, _ = build_model(load_fixture(FIXTURE))
+        model = model.to(gpu).train()
+        s, e = shard_bounds(GB_TRAIN, 2, r)
+        _shard_grads(model, x[s:e], y[s:e], 100 + r)
+        per.append({n: p.grad.detach().cpu() for n, p in model.named_parameters()})
+    assert set(ddp) == set(per[0])
+    worst = 0.0
+    for n in ddp:
+        ref = (per[0][n] + per[1][n]) / 2  # DDP: every rank's gradient averaged over the world
+        scale = ref.abs().max().item() + 1e-30
+        err = (ddp[n] - ref).abs().max().item()
+        worst = max(worst, err / scale)
+        assert err <= 1e-6 * scale, f"{n}: max|d grad| {err:.3e} vs max|grad| {scale:.3e}"
+        assert ref.abs().sum().item() > 0, n
+    print(f"DDP world 2: {len(ddp)} parameter gradients, worst relative difference {worst:.2e}")
+
+
+# ---------------------------------------------------------------- sharded eval engine
+GB_EVAL = 7  # ragged: shards of 4 and 3 samples
+
+
+def _calib_batches(rank, world):
+    from qnn import synthetic
+    from qnn.dist import shard_bounds
+    s, e = shard_bounds(GB_EVAL, world, rank)
+    return [synthetic.input_batch((GB_EVAL, 3, 32, 32), 500 + j)[s:e] for j in range(2)]
+
+
+def _calibrate(model, batches, dev):
+    from qnn.quantize import set_measure_mode
+    set_measure_mode(model, True)
+    model.train()
+    with torch.no_grad():
+        for b in batches:
+            model(b.to(dev))
+    set_measure_mode(model, False)
+    model.eval()
+
+
+def _eval_worker(rank, world, port, out):
+    dist = _init(rank, world, port)
+    from conftest import load_fixture
+    from fixtures_util import build_model
+    from qnn import synthetic
+    from qnn.dist import ShardedInference, allreduce_calibration, shard_bounds
+    from qnn.engine import Engine
+    dev = torch.device("cuda:0")
+    model, _ = build_model(load_fixture(FIXTURE))
+    model = model.to(dev)
+    batches = _calib_batches(rank, world)
+    _calibrate(model, batches, dev)
+    allreduce_calibration(model, samples=batches[0].shape[0])
+    s, e = shard_bounds(GB_EVAL, world, rank)
+    eng = Engine(model, batch=e - s)
+    runner = ShardedInference(eng, GB_EVAL)
+    x = synthetic.input_batch((GB_EVAL, 3, 32, 32), 600).to(dev)
+    logits = runner(x[s:e])
+    if rank == 0:
+        torch.save({"logits": logits.detach().cpu(),
+                    "state": {k: v.detach().cpu() for k, v in model.state_dict().items()}}, out)
+    else:
+        assert logits is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_engine_world2_device(gpu, tmp_path):
+    from conftest import load_fixture
+    from fixtures_util import build_model
+    from qnn import synthetic
+    from qnn.engine import Engine
+    from qnn.quantize import QuantMeasure, RangeBN
+    out = str(tmp_path / "eval.pt")
+    _spawn(_eval_worker, (out,))
+    got = torch.load(out, weights_only=True)
+    # single process: each shard's calibration on its own, merged with the sample weights
+    states = []
+    for r in range(2):
+        model, _ = build_model(load_fixture(FIXTURE))
+        model = model.to(gpu)
+        _calibrate(model, _calib_batches(r, 2), gpu)
+        states.append(model)
+    w = [b[0].shape[0] for b in (_calib_batches(0, 2), _calib_batches(1, 2))]
+    merged = states[0]
+    with torch.no_grad():
+        for (n, m0), m1 in zip(merged.named_modules(), [m for _, m in states[1].named_modules()]):
+            names = (("running_min", "running_max", "running_mean", "running_var") if isinstance(m0, QuantMeasure)
+                     else ("running_mean", "running_var") if isinstance(m0, RangeBN) else ())
+            for k in names:
+                a, b = getattr(m0, k), getattr(m1, k)
+                v = (a.double() * w[0] + b.double() * w[1]) / (w[0] + w[1])
+                a.copy_(v)
+                assert torch.equal(got["state"][n + "." + k if n else k], a.cpu()), f"merged {n}.{k}"
+    eng = Engine(merged, batch=GB_EVAL)
+    ref = eng(synthetic.input_batch((GB_EVAL, 3, 32, 32), 600).to(gpu)).clone().cpu()
+    assert got["logits"].shape == ref.shape
+    ndiff = int((got["logits"] != ref).sum())
+    assert ndiff == 0, f"{ndiff} gathered logits differ from the single-process engine"

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Phase breakdown of the resident-band conv kernel (qconv_rb.hip) from its QNN_STAMP build.
+"""Phase breakdown of the resident-band conv kernels from their QNN_STAMP builds.
 
     QNN_LIB=quantized.pytorch_amd/qnn/libqnn_hip_stamp_rb.so python tools/rb_stamps.py [--tiles 26 29]
+    QNN_LIB=quantized.pytorch_amd/qnn/libqnn_hip_rbpstamp.so python tools/rb_stamps.py --kernel rbp --tiles 40 41
 
 For each ResNet layer picked (engine launch of the fused forward, its real epilogue kind) the
 launch is forced onto each resident-band configuration and run; per wave: cycles until the
@@ -27,6 +28,9 @@ from qnn import _lib, synthetic  # noqa: E402
 from qnn.engine import Engine  # noqa: E402
 
 
+KERNEL = "rb"
+
+
 def run(eng, idx, d, e, tile, reps):
     d.tile = tile + 1
     if not Engine._plan_ok(d, e):
@@ -46,23 +50,34 @@ def run(eng, idx, d, e, tile, reps):
     torch.cuda.synchronize()
     us = ev[0].elapsed_time(ev[1]) * 1e3
     lib = _lib.load()
-    fn = lib.qnn_debug_stamps_rb
+    fn = getattr(lib, "qnn_debug_stamps_" + KERNEL)
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     W = 8
-    n = min(nblk.value, (1 << 18) // (8 * W))
-    buf = np.zeros(n * W * 8, dtype=np.uint64)
+    S = 16 if KERNEL == "rbp" else 8  # stamp slots per wave
+    n = min(nblk.value, (1 << 18) // (S * W))
+    buf = np.zeros(n * W * S, dtype=np.uint64)
     assert fn(buf.ctypes.data, buf.nbytes) == 0
     d.tile = 0
-    return us, nblk.value, buf.reshape(n, W, 8).astype(np.float64)
+    return us, nblk.value, buf.reshape(n, W, S).astype(np.float64)
 
 
 def report(tag, us, nblk, w):
     cyc = w[:, :, 2:8]
     mean = cyc.mean((0, 1))
     tot = cyc.sum(-1).mean()
-    names = ["band", "k-loop", "sums", "staging", "epi", "drain"]
+    names = (["band", "k-loop", "sums", "staging", "epi", "drain"] if KERNEL == "rb" else
+             ["chunk0", "k-loop", "sums", "epidata", "epi", "drain"])
     print(f"== {tag}: {us:.1f} us (stamped build), blocks={nblk}, wave-cycles {tot:.0f}: " +
           "  ".join(f"{a}={m:.0f} ({100 * m / tot:.1f}%)" for a, m in zip(names, mean)))
+    if KERNEL == "rbp":  # the two teams (waves 0-3 at priority 2, 4-7 at 0)
+        for tm in (0, 1):
+            c = cyc[:, 4 * tm:4 * tm + 4]
+            cum = np.cumsum(c.mean((0, 1)))
+            print(f"   team {tm}: " + "  ".join(f"{a}={m:.0f}" for a, m in zip(names, c.mean((0, 1)))) +
+                  "   cumulative end of each phase: " + " ".join(f"{x:.0f}" for x in cum))
+        pro = w[:, 4:8, 8:15].mean((0, 1))
+        print("   team 1 prologue (cycles from start): issued {:.0f}, chunks landed {:.0f} {:.0f} {:.0f} {:.0f}, "
+              "pixel sums {:.0f}, epilogue data staged {:.0f}".format(*pro))
     rs = w[:, 0, 0] - w[:, 0, 0].min()
     re_ = w[:, 0, 1] - w[:, 0, 0].min()
     life = re_ - rs
@@ -78,7 +93,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--tiles", nargs="*", type=int, default=None)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--kernel", choices=("rb", "rbp"), default="rb")
+    ap.add_argument("--only3x3", default="")
     a = ap.parse_args()
+    global KERNEL
+    KERNEL = a.kernel
     dev = torch.device("cuda:0")
     _lib.load()
     model = bench.build(dev, a.depth)
