@@ -282,8 +282,7 @@ def main():
     model = build(device, args.depth, arch=args.model)
     total_ops, mfma_ops = model_ops(model, args.batch)
     from qnn import synthetic
-    from qnn.engine import Engine
-    engine = Engine(model, batch=args.batch)
+    engine = qdist.build_engine(model, args.batch)  # rank 0's autotuned tiles on every rank
     engine.input.copy_(synthetic.input_batch((args.batch, 3, 224, 224), 1234 + rank).to(device))
     runner = qdist.ShardedInference(engine, args.batch * world)
 

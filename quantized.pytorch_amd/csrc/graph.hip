@@ -237,7 +237,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   const int tc = threadIdx.x % ct, tp = threadIdx.x / ct;
   if (tp >= per_blk) return;  // c/CPT not a divisor of 256: idle tail threads
   const int nxg = (wo + R - 1) / R, total = rows * nxg, cb = CPT * tc;
-  if (blockIdx.x * per_blk + tp >= total) return;
+  // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
+  // one), so logical block L = the bijective XCD-major index of b gives each XCD a contiguous
+  // range of L -- adjacent output rows, whose 3x3 windows share input rows, are then computed
+  // on one XCD and the halo rows are served by its L2 instead of being fetched once per XCD
+  int blk;
+  {
+    const int nb = gridDim.x, bb = blockIdx.x, xcd = bb & 7, q = nb >> 3, r = nb & 7;
+    blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bb >> 3);
+  }
+  if (blk * per_blk + tp >= total) return;
   // every per-channel quantity as packed pairs (channels 2p, 2p+1): v_pk_fma/mul/add run the
   // same IEEE fp32 op per element as the scalar form, so the results are bitwise unchanged
   f2 wv[K * K][P];
@@ -286,8 +295,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   // once per thread and reused across all of its groups
   const int step = gridDim.x * per_blk;
   LT v[K][NCOL];
-  if (QNN_DW_PF) load(blockIdx.x * per_blk + tp, v);
-  for (int pg = blockIdx.x * per_blk + tp; pg < total; pg += step) {
+  if (QNN_DW_PF) load(blk * per_blk + tp, v);
+  for (int pg = blk * per_blk + tp; pg < total; pg += step) {
     const int row = pg / nxg, xg = pg - row * nxg;
     const int img = row / ho, oy = row - img * ho;
     const int ox0 = xg * R;

@@ -197,23 +197,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     // team 1 waits for them itself, counted (wait_vmcnt_rt), before anything reads the band
     asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(dst), "v"(off), "s"(x) : "memory", "m0");
   };
-  // (the memory clobbers keep every weight load in program order around the pieces: the
-  // counted vmcnt waits below rely on exactly which loads follow them)
-  auto issue_chunk = [&](int gch) {  // planes 2gch, 2gch + 1 over team 1's four waves
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    for (int k = tw; k < 2 * g.ppp; k += 4) {
-      const int hi = k >= g.ppp;
-      issue_piece(k - (hi ? g.ppp : 0), 2 * gch + hi);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
+  // Chunk gch = planes 2gch, 2gch + 1 = 2 ppp pieces, NPW = ppp / 4 per wave (geometry: ppp % 4
+  // == 0); this wave's piece i of it is piece k = wave + 8 i.
+  auto issue_own = [&](int gch, int i) {
+    const int k = wave + 8 * i, hi = k >= g.ppp;
+    issue_piece(k - (hi ? g.ppp : 0), 2 * gch + hi);
   };
   // sum_valid(q'_x), part 1: once a wave's pieces of chunk gch have landed, each lane sums the
   // 16 bytes it moved itself (v_dot4 against 1s), the two halves of a pixel combine, and the
   // pixel's channel sum accumulates in LDS (exact integer adds in any order)
   auto sum_chunk = [&](int gch) {
-    for (int k = tw; k < 2 * g.ppp; k += 4) {
+    for (int k = wave; k < 2 * g.ppp; k += 8) {
       const int hi = k >= g.ppp, r = k - (hi ? g.ppp : 0);
       v4i a;
       asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
@@ -230,17 +224,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     }
   };
 
-  // ---- the block's epilogue data by LDS-DMA (qconv_common.h stage_epi's layout), by team 1
+  // LDS-DMA in inline asm (a lane's bytes land at the wave-uniform LDS address + lane * size):
+  // invisible to the compiler's vmcnt bookkeeping, waited for explicitly (wait_vmcnt<0> before
+  // the epilogue), so the K loop's weight waits stay counted
+  auto dma4 = [&](const void* src, int8_t* ldst) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+  };
+  auto dma16 = [&](const void* src, int8_t* ldst) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+  };
+  // ---- the team's epilogue data by LDS-DMA (qconv_common.h stage_epi's layout; this team's
+  // 64-channel chunks k = 2 team, 2 team + 1)
   const bool lut_on = EK == EK_LUT && g.lut;
-  auto stage_all = [&] {
+  auto stage_team = [&] {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const int cmax = d.cout - 1;
     const int nvec = (EK != EK_NCHW && e.bn_mean) ? 7 : 3;
-    const int nf = (nvec + e.nclass) * 4;
+    const int nf = (nvec + e.nclass) * 2;
     int8_t* dst = smem + p.epi_off;
     for (int jb = tw; jb < nf; jb += 4) {
-      const int v = jb >> 2, k = jb & 3;
+      const int v = jb >> 1, k = 2 * team + (jb & 1);
       const int arr = v < nvec ? v : 7 + (v - nvec);
       int c = c0 + 64 * k + lane;
       c = c < cmax ? c : cmax;
@@ -262,15 +268,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
         case 6: src = e.bn_bq; break;
         default: src = e.table + (int64_t)(arr - 7) * d.cout; break;
       }
-      __builtin_amdgcn_global_load_lds((const void*)(src + c), (lds_ptr_t)(dst + 4 * (arr * BM + 64 * k)), 4, 0, 0);
+      dma4(src + c, dst + 4 * (arr * BM + 64 * k));
     }
     if (lut_on) {
       int8_t* lut = dst + 4 * (7 + e.nclass) * BM;
-      for (int jl = tw; jl < BM / 4; jl += 4) {
+      for (int jl = 32 * team + tw; jl < 32 * team + 32; jl += 4) {
         int c = c0 + 4 * jl + (lane >> 4);
         c = c < cmax ? c : cmax;
-        __builtin_amdgcn_global_load_lds((const void*)(e.lut + (int64_t)c * 256 + 16 * (lane & 15)),
-                                         (lds_ptr_t)(lut + 1024 * jl), 16, 0, 0);
+        dma16(e.lut + (int64_t)c * 256 + 16 * (lane & 15), lut + 1024 * jl);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
   const int G = d.cp / 64, taps = p.taps;
   v4i fa[DA][TM];
   int lg = 0, lt = 0;  // the next step to load
-  auto load_a = [&](v4i (&dst)[TM]) {
+  auto load_a = [&](v4i (&dst)[TM]) __attribute__((always_inline)) {
     const int8_t* base = wblk + lt * d.cp + 64 * lg;
 #pragma unroll
     for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const v4i*>(base + aoff[i]);
@@ -313,75 +318,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     }
   };
 
-  // ---- prologue.  Team 1 is the band's loader: it issues every chunk, then -- before its
-  // own K loop -- waits for them in order, publishing each (LDS counter) and summing its bytes,
-  // sums each output pixel's receptive field, and stages the epilogue data.  Team 0 computes
-  // from the first published chunk on, alone on the matrix pipes meanwhile: that head start is
-  // the stagger that lets its epilogue run beside team 1's K loop.  (A wave's vmcnt is in
-  // order, so a wave that both streamed the band and loaded weights would wait for the band
-  // at its first weight wait; team 0 loads only weights.)
-  const int ppc = g.ppp / 2;  // pieces per team-1 wave per chunk (geometry: ppp even)
-  // (no load result may be pending across the join below: the waitcnt pass would then wait
-  // for every piece in flight before team 1's publishing loop)
+  // ---- prologue: every wave issues its pieces of chunk 0 and the first DA - 1 steps' weights,
+  // publishes the chunk once its pieces landed (the vmcnt leaves the weight loads in flight)
+  // and sums the bytes it moved
+  const int NPW = g.ppp / 4;
   for (int i = tid; i < SYNC_INTS + C::BN; i += NT) s_sync[i] = 0;
   for (int i = tid; i < g.nbp; i += NT) s_ps[i] = 0;
-  if (team == 1)
-    for (int gch = 0; gch < G; ++gch) issue_chunk(gch);
   // the only workgroup barrier (the counters are zero).  A raw s_barrier: __syncthreads()'s
-  // release fence would wait for every LDS-DMA piece in flight (vmcnt(0)), i.e. the whole band
+  // release fence would also wait for every VMEM op in flight
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (team == 1) {
 #if QNN_STAMP
-    RBP_TS(tp[0]);
+  RBP_TS(tp[0]);
 #endif
-    for (int gch = 0; gch < G; ++gch) {
-      wait_vmcnt_rt((G - 1 - gch) * ppc);  // this wave's pieces of chunk gch (younger ones may fly)
-#if QNN_STAMP
-      if (gch < 4) RBP_TS(tp[1 + gch]);
-#endif
-      arrive(&s_sync[gch], lane);
-      sum_chunk(gch);
-    }
-    if (tw == 0 && lane < d.ho + d.wo)  // the border-class tables, by wave 4
-      s_hc[lane] = lane < d.ho ? e.hcls[lane] * e.nwc : e.wcls[lane - d.ho];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    arrive(&s_sync[20], lane);
-    poll(&s_sync[20], 4);  // every band-pixel sum is in
-    // sum_valid(q'_x), part 2: one lane per output pixel sums its taps of the band-pixel sums
-    // (padding codes are 0, so this is the receptive field's exact sum)
-    for (int q = 64 * tw + lane; q < C::BN; q += 256) {
-      int qq = q < npx_blk ? q : npx_blk - 1;
-      const int rr = qq / d.wo, col = qq - rr * d.wo;
-      const int r = r0 + rr, n = r / d.ho, ho = r - n * d.ho;
-      const int b0 = (n * d.hp + ho * d.sh - R0) * g.wb + col;
-      int sm = 0;
-      for (int tt = 0; tt < taps; ++tt) sm += s_ps[b0 + tap_off(tt)];
-      s_sum[q] = sm;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    arrive(&s_sync[16], lane);
-#if QNN_STAMP
-    RBP_TS(tp[5]);
-#endif
-    stage_all();
+  for (int i = 0; i < NPW; ++i) issue_own(0, i);
 #pragma unroll
-    for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
-    wait_vmcnt<(DA - 1) * TM>();  // the staging landed (only the weight loads may fly)
+  for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
 #if QNN_STAMP
-    RBP_TS(tp[6]);
+  RBP_TS(tp[1]);
 #endif
-    arrive(&s_sync[17], lane);
-  } else {
-#pragma unroll
-    for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
-  }
+  wait_vmcnt<(DA - 1) * TM>();
+#if QNN_STAMP
+  RBP_TS(tp[2]);
+#endif
+  arrive(&s_sync[0], lane);
+  sum_chunk(0);
+#if QNN_STAMP
+  RBP_TS(tp[3]);
+#endif
 
   v4i acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
-  auto step = [&](auto slotc, int gk, int tap) {
+  auto step = [&](auto slotc, int gk, int tap) __attribute__((always_inline)) {
     constexpr int SL = decltype(slotc)::value;
     const int boff = 2 * gk * g.pl + 32 * tap_off(tap);
     v4i fb[TN];
@@ -402,23 +372,60 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
     // DESIGN.md §4, tools/asm_mfma_war_check.py)
     load_a(fa[(SL + DA - 1) % DA]);
   };
-
+  // The next chunk's pieces, one per wave every second step (after that step's weight loads:
+  // taps 1 and 3), published at the start of tap 6: every VMEM op issued after the last piece
+  // by then is one of the 2 TM weight loads of taps 4 and 5, so a counted vmcnt(2 TM) covers
+  // it, and the compiler's own weight waits before tap 6 are for loads issued before it -- the
+  // DMA never stalls the K loop unless a piece takes two steps to land.  (Geometry: NPW <= 2,
+  // taps == 9.)  Straight-line per group: no VMEM op the compiler sees but the weight loads.
+  if (G == 1) arrive(&s_sync[20], lane);
 #pragma nounroll
   for (int gk = 0; gk < G; ++gk) {
-    poll(&s_sync[gk], 4);  // chunk gk landed (all of team 1's pieces)
+    poll(&s_sync[gk], 8);  // chunk gk landed (every wave's pieces)
 #if QNN_STAMP
     if (gk == 0) RBP_TS(ts1);
 #endif
+    const bool more = gk + 1 < G;
 #pragma nounroll
     for (int t0 = 0; t0 < taps; t0 += 3) {
+      if (more && t0 == 6) {
+        wait_vmcnt<2 * TM>();
+        arrive(&s_sync[gk + 1], lane);
+        sum_chunk(gk + 1);
+        if (gk + 2 == G) arrive(&s_sync[20], lane);  // this wave's band-pixel sums are all in
+      }
       step(std::integral_constant<int, 0>{}, gk, t0);
+      if (more && t0 == 3 && NPW > 1) issue_own(gk + 1, 1);
       step(std::integral_constant<int, 1>{}, gk, t0 + 1);
+      if (t0 == 0) {
+        if (more) issue_own(gk + 1, 0);
+        else stage_team();  // the team's epilogue data, behind every chunk
+      }
       step(std::integral_constant<int, 2>{}, gk, t0 + 2);
     }
   }
 #if QNN_STAMP
   RBP_TS(ts2);
 #endif
+  // ---- sum_valid(q'_x), part 2, by the first team out of its K loop (team 0, priority): one
+  // lane per output pixel sums its taps of the band-pixel sums (padding codes are 0, so this is
+  // the receptive field's exact sum)
+  if (team == 0) {
+    if (tw == 0 && lane < d.ho + d.wo)  // the border-class tables
+      s_hc[lane] = lane < d.ho ? e.hcls[lane] * e.nwc : e.wcls[lane - d.ho];
+    poll(&s_sync[20], 8);
+    for (int q = 64 * tw + lane; q < C::BN; q += 256) {
+      int qq = q < npx_blk ? q : npx_blk - 1;
+      const int rr = qq / d.wo, col = qq - rr * d.wo;
+      const int r = r0 + rr, n = r / d.ho, ho = r - n * d.ho;
+      const int b0 = (n * d.hp + ho * d.sh - R0) * g.wb + col;
+      int sm = 0;
+      for (int tt = 0; tt < taps; ++tt) sm += s_ps[b0 + tap_off(tt)];
+      s_sum[q] = sm;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    arrive(&s_sync[16], lane);
+  }
   poll(&s_sync[16], 4);  // the pixel sums
   int sumq[TN];
 #pragma unroll
@@ -426,9 +433,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
 #if QNN_STAMP
   RBP_TS(ts3);
 #endif
-  // the epilogue data (staged by team 1 in its prologue) and this wave's tail weight loads
+  // the team's epilogue data (staged by its four waves) and this wave's tail weight loads
   wait_vmcnt<0>();
-  poll(&s_sync[17], 4);
+  arrive(&s_sync[17 + team], lane);
+  poll(&s_sync[17 + team], 4);
 #if QNN_STAMP
   RBP_TS(ts4);
 #endif
@@ -522,7 +530,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
 // one block per CU, else the first that fits.  Returns the LDS bytes or -1.
 static int geometry(const Params& p, int BM, int BN, int ek, Geo& g) {
   const qnn_conv_desc& d = p.d;
-  if (p.taps < 6 || p.taps % 3 != 0 || d.kmask || d.cp % 64 != 0 || d.cp > 1024) return -1;
+  if (p.taps != 9 || d.kmask || d.cp % 64 != 0 || d.cp > 1024) return -1;
   const int G = d.cp / 64;
   if (d.sh != d.sw || (d.sh != 1 && d.sh != 2)) return -1;
   if (d.kpad < p.taps * d.cp) return -1;
@@ -538,14 +546,14 @@ static int geometry(const Params& p, int BM, int BN, int ek, Geo& g) {
     g.nbp = nbrows * g.wb;
     g.pl = (int)cdiv((int64_t)g.nbp * 32, 1024) * 1024;
     g.ppp = g.pl / 1024;
-    if (g.ppp % 2 != 0) g.pl += 1024, g.ppp += 1;  // even: every team-1 wave moves ppp / 2 pieces a chunk
+    if (g.ppp % 4 != 0) g.ppp += 4 - g.ppp % 4, g.pl = 1024 * g.ppp;  // every wave moves ppp / 4 pieces a chunk
     g.sync_off = npl * g.pl;
     g.ps_off = g.sync_off + 4 * (SYNC_INTS + BN);
     g.cls_off = g.ps_off + 4 * g.nbp;
     const int epi_off = (g.cls_off + 4 * (d.ho + d.wo) + 15) & ~15;
     g.lut = lut;
     g.lds = epi_off + epi_vec + (lut ? 256 * BM : 0);
-    if (G * (g.ppp / 2) > 60) return -1;  // team 1's pieces in flight (vmcnt counts to 63)
+    if (g.ppp / 4 > 2) return -1;  // the next chunk is issued and published within a group
     return g.lds <= LDS_MAX ? epi_off : -1;
   };
   const int nby = (int)cdiv(d.cout, BM);

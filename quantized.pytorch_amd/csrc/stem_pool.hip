@@ -4,7 +4,10 @@
 // in one kernel.  The unfused path writes the stem's full-resolution RangeBN codes to HBM and
 // reads them back in qnn_maxpool_bn (103 MB each way at ResNet-18 b128); here they live in LDS.
 //
-// A block owns PR pooled rows of one image (all pooled columns, all 64 channels):
+// The kernel is persistent: one block per CU walks the items (PR pooled rows of one image each;
+// all pooled columns, all 64 channels), staging the epilogue data and code tables once and
+// double-buffering the band: item i + 1's band lands by LDS-DMA under item i's tiles and pooling.
+// Per item:
 //  0. the padded space-to-depth input rows those stem rows read -- one contiguous stretch of
 //     the NHWC16 codes -- land in LDS by LDS-DMA (the BAND), with the epilogue data and tables;
 //  1. the stem rows its windows read (2*PR + 1, fewer at the image edge) are computed with
@@ -58,7 +61,8 @@ struct Pool {
   qnn_code_out c0;
   const int8_t* lut1;
   qnn_code_out c1;
-  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc, lds_band, lds_zero;  // LDS offsets
+  int nitems;            // n * nrg
+  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc, lds_band, lds_band_bytes, lds_zero;  // LDS offsets
 };
 
 template <int KS, bool MASKED>
@@ -69,24 +73,42 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   const qnn_epilogue& e = p.e;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int img = blockIdx.x / pl.nrg, pr0 = (blockIdx.x - img * pl.nrg) * PR;
-  const int npr = min(PR, pl.ho - pr0);
-  // stem rows the windows of pooled rows [pr0, pr0 + npr) read (MaxPool2d(3, 2, 1))
-  const int sr_lo = max(2 * pr0 - 1, 0), sr_hi = min(2 * (pr0 + npr - 1) + 1, d.ho - 1);
-  const int npx = (sr_hi - sr_lo + 1) * d.wo, ntile = (npx + 15) >> 4;
 
-  // ---- the band: padded input rows [R0, R0 + nbr) of this image, one contiguous stretch of
-  // nbr * wp * cp bytes, by 1 KiB LDS-DMA pieces (past its end: the zero page)
-  const int R0 = img * d.hp + sr_lo * d.sh, nbr = (sr_hi - sr_lo) * d.sh + d.kh;
-  const int band_bytes = nbr * d.wp * d.cp;
-  {
-    const int64_t src0 = (int64_t)R0 * d.wp * d.cp;
-    for (int pc = wave; pc * 1024 < band_bytes && QNN_SP_ABLATE != 4; pc += W) {
+  // item -> (image, first pooled row, stem rows [sr_lo, sr_hi], padded input rows of its band)
+  struct Item {
+    int img, pr0, npr, sr_lo, sr_hi, npx, ntile, R0, band_bytes;
+  };
+  auto item = [&](int it) {
+    Item q;
+    q.img = it / pl.nrg;
+    q.pr0 = (it - q.img * pl.nrg) * PR;
+    q.npr = min(PR, pl.ho - q.pr0);
+    // stem rows the windows of pooled rows [pr0, pr0 + npr) read (MaxPool2d(3, 2, 1))
+    q.sr_lo = max(2 * q.pr0 - 1, 0);
+    q.sr_hi = min(2 * (q.pr0 + q.npr - 1) + 1, d.ho - 1);
+    q.npx = (q.sr_hi - q.sr_lo + 1) * d.wo;
+    q.ntile = (q.npx + 15) >> 4;
+    q.R0 = q.img * d.hp + q.sr_lo * d.sh;
+    q.band_bytes = ((q.sr_hi - q.sr_lo) * d.sh + d.kh) * d.wp * d.cp;
+    return q;
+  };
+  // ---- the band of an item: padded input rows [R0, R0 + nbr) of its image, one contiguous
+  // stretch of nbr * wp * cp bytes, by 1 KiB LDS-DMA pieces (past its end: the zero page), in
+  // inline asm -- invisible to the compiler's waitcnt bookkeeping, which would otherwise fence
+  // every LDS read of the tile loop behind it; waited for explicitly (vmcnt(0) per item)
+  auto issue_band = [&](const Item& q, int buf) {
+    const int64_t src0 = (int64_t)q.R0 * d.wp * d.cp;
+    const uint32_t dst0 = (uint32_t)(uintptr_t)(smem + pl.lds_band + buf * pl.lds_band_bytes);
+    for (int pc = wave; pc * 1024 < q.band_bytes && QNN_SP_ABLATE != 4; pc += W) {
       const int o = pc * 1024 + 16 * lane;
-      const int64_t src = o < band_bytes ? src0 + o : (int64_t)d.zero_off;
-      __builtin_amdgcn_global_load_lds((const void*)(x + src), (lds_ptr_t)(smem + pl.lds_band + pc * 1024), 16, 0, 0);
+      const int64_t src = o < q.band_bytes ? src0 + o : (int64_t)d.zero_off;
+      const uint32_t m = __builtin_amdgcn_readfirstlane(dst0 + pc * 1024);
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(x + src) : "memory", "m0");
     }
-  }
+  };
+  int it = blockIdx.x;
+  if (it >= pl.nitems) return;
+  issue_band(item(it), 0);
   // ---- staged once: epilogue vectors + border table (stage_epi), code tables, border classes
   stage_epi<Cfg, EK_BNCODE>(p, x, smem, 0, wave, lane);
   auto stage_lut = [&](const int8_t* lut, int off) {
@@ -116,20 +138,8 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
     if constexpr (MASKED) ones[s] = *reinterpret_cast<const v4i*>(d.kmask + 64 * s + 16 * g);
     else ones[s] = (v4i){0x01010101, 0x01010101, 0x01010101, 0x01010101};
   }
-  auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
-    int q = t * 16 + (lane & 15);
-    q = q < npx ? q : npx - 1;  // past the rows: the last pixel again (its store is skipped)
-    lr = q / d.wo;
-    col = q - lr * d.wo;
-    const int base = pl.lds_band + (lr * d.sh * d.wp + col * d.sw) * d.cp;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-      fb[s] = *reinterpret_cast<const v4i*>(smem + (doff[s] >= 0 ? base + doff[s] : pl.lds_zero));
-  };
-
-  wait_vmcnt<0>();  // band, staged data, tables and weights
+  wait_vmcnt<0>();  // staged data, tables, weights (and the first band)
   __syncthreads();
-
   const float* s_f = reinterpret_cast<const float*>(smem);
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
   float4 sw[TM], bw[TM], bi[TM];
@@ -141,116 +151,137 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
     bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * C + cl);
   }
   uint8_t* s_codes = reinterpret_cast<uint8_t*>(smem + pl.lds_codes);
-
-  // ---- 1. stem tiles: wave w takes tiles w, w + W, ...; the next tile's fragments are read
-  //         from the band before this one's MFMAs
-  v4i fnx[KS];
-  int nlr, ncol;
-  if (wave < ntile) load_b(wave, fnx, nlr, ncol);
-  for (int t = wave; t < ntile; t += W) {
-    v4i fb[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) fb[s] = fnx[s];
-    const int lr = nlr, col = ncol;
-    if (t + W < ntile) load_b(t + W, fnx, nlr, ncol);
-    v4i acc[TM], sacc = (v4i){0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i] = (v4i){0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (QNN_SP_ABLATE == 1) {
-        asm volatile("" ::"v"(fb[s]));
-        sacc[0] += fb[s][0];
-        continue;
-      }
-      sacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], sacc, 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], acc[i], 0, 0, 0);
-    }
-    if (QNN_SP_ABLATE == 2) {
-      int z = sacc[0];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) z ^= acc[i][0] ^ acc[i][1] ^ acc[i][2] ^ acc[i][3];
-      if (t * 16 + (lane & 15) < npx) *reinterpret_cast<int*>(s_codes + (lr * d.wo + col) * C + 4 * g) = z;
-      continue;
-    }
-    const int pc = s_hc[sr_lo + lr] + s_hc[d.ho + col];
-    const f2 p2 = {(float)sacc[0], (float)sacc[0]};
-    const bool ok = t * 16 + (lane & 15) < npx;
-    uint8_t* dst = s_codes + (lr * d.wo + col) * C + 4 * g;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int cl = 16 * i + 4 * g;
-      const float4 tb = *reinterpret_cast<const float4*>(s_f + (7 + pc) * C + cl);
-      const v4i& a = acc[i];
-      const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
-      // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
-      const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
-                    (f2){bi[i].x, bi[i].y};
-      const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
-                    (f2){bi[i].z, bi[i].w};
-      const int kb = pack4(qclamp2(v0, bnp) + MAGIC_U8, qclamp2(v1, bnp) + MAGIC_U8);  // EK_BNCODE
-      if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb;
-    }
-  }
   // pool direction per channel: 0xff where relu o RangeBN is non-increasing (sq * wq < 0)
   uint8_t* s_dir = reinterpret_cast<uint8_t*>(smem + pl.lds_dir);
   if (tid < C) s_dir[tid] = (s_f[4 * C + tid] * s_f[5 * C + tid]) < 0.f ? 0xff : 0;
-  __syncthreads();
-
-  // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest
   const int ct = (C + 31) >> 5;
-  for (int it = tid; it < npr * pl.wo * 4 && QNN_SP_ABLATE != 3; it += NT) {
-    const int cg = it & 3, pxi = it >> 2;
-    const int prl = pxi / pl.wo, pc = pxi - prl * pl.wo;
-    const int oy = pr0 + prl, cb = 16 * cg;
-    const uint4 dm = *reinterpret_cast<const uint4*>(s_dir + cb);
-    uint4 best = make_uint4(0, 0, 0, 0);
+
+  for (int buf = 0; it < pl.nitems; it += gridDim.x, buf ^= 1) {
+    const Item q = item(it);
+    // this item's band landed (every wave's pieces) and the previous item's pooling is done
+    // with the codes: then the next item's band DMA goes into the other buffer, whose last
+    // reader (the previous item's tiles) finished before the previous barrier
+    wait_vmcnt<0>();
+    __syncthreads();
+    if (it + (int)gridDim.x < pl.nitems) issue_band(item(it + gridDim.x), buf ^ 1);
+    const int band = pl.lds_band + buf * pl.lds_band_bytes;
+    auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
+      int qq = t * 16 + (lane & 15);
+      qq = qq < q.npx ? qq : q.npx - 1;  // past the rows: the last pixel again (its store is skipped)
+      lr = qq / d.wo;
+      col = qq - lr * d.wo;
+      const int base = band + (lr * d.sh * d.wp + col * d.sw) * d.cp;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int sy = 2 * oy - 1 + r;
+      for (int s = 0; s < KS; ++s)
+        fb[s] = *reinterpret_cast<const v4i*>(smem + (doff[s] >= 0 ? base + doff[s] : pl.lds_zero));
+    };
+
+    // ---- 1. stem tiles: wave w takes tiles w, w + W, ...; the next tile's fragments are read
+    //         from the band before this one's MFMAs
+    v4i fnx[KS];
+    int nlr = 0, ncol = 0;
+    if (wave < q.ntile) load_b(wave, fnx, nlr, ncol);
+    for (int t = wave; t < q.ntile; t += W) {
+      v4i fb[KS];
 #pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) {
-        const int sx = 2 * pc - 1 + s2;
-        // MaxPool2d pads with -inf: an out-of-image tap reads a clamped pixel and is masked
-        // to 0, the identity of the folded-code max
-        const bool okt = sy >= 0 && sy < d.ho && sx >= 0 && sx < d.wo;
-        const int ly = min(max(sy, sr_lo), sr_hi) - sr_lo, lx = min(max(sx, 0), d.wo - 1);
-        const uint4 v = *reinterpret_cast<const uint4*>(s_codes + (ly * d.wo + lx) * C + cb);
-        const uint32_t msk = okt ? 0xffffffffu : 0u;
-        best.x = max_u8x4(best.x, (v.x ^ dm.x) & msk);
-        best.y = max_u8x4(best.y, (v.y ^ dm.y) & msk);
-        best.z = max_u8x4(best.z, (v.z ^ dm.z) & msk);
-        best.w = max_u8x4(best.w, (v.w ^ dm.w) & msk);
+      for (int s = 0; s < KS; ++s) fb[s] = fnx[s];
+      const int lr = nlr, col = ncol;
+      if (t + W < q.ntile) load_b(t + W, fnx, nlr, ncol);
+      v4i acc[TM], sacc = (v4i){0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i] = (v4i){0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (QNN_SP_ABLATE == 1) {
+          asm volatile("" ::"v"(fb[s]));
+          sacc[0] += fb[s][0];
+          continue;
+        }
+        sacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], sacc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], acc[i], 0, 0, 0);
+      }
+      if (QNN_SP_ABLATE == 2) {
+        int z = sacc[0];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) z ^= acc[i][0] ^ acc[i][1] ^ acc[i][2] ^ acc[i][3];
+        if (t * 16 + (lane & 15) < q.npx) *reinterpret_cast<int*>(s_codes + (lr * d.wo + col) * C + 4 * g) = z;
+        continue;
+      }
+      const int pc = s_hc[q.sr_lo + lr] + s_hc[d.ho + col];
+      const f2 p2 = {(float)sacc[0], (float)sacc[0]};
+      const bool ok = t * 16 + (lane & 15) < q.npx;
+      uint8_t* dst = s_codes + (lr * d.wo + col) * C + 4 * g;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cl = 16 * i + 4 * g;
+        const float4 tb = *reinterpret_cast<const float4*>(s_f + (7 + pc) * C + cl);
+        const v4i& a = acc[i];
+        const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
+        // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
+        const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
+                      (f2){bi[i].x, bi[i].y};
+        const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
+                      (f2){bi[i].z, bi[i].w};
+        const int kb = pack4(qclamp2(v0, bnp) + MAGIC_U8, qclamp2(v1, bnp) + MAGIC_U8);  // EK_BNCODE
+        if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb;
       }
     }
-    const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
-    const int64_t m = ((int64_t)img * pl.ho + oy) * pl.wo + pc;
-    if (pl.out_code) {
+    __syncthreads();
+
+    // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest
+    for (int pi = tid; pi < q.npr * pl.wo * 4 && QNN_SP_ABLATE != 3; pi += NT) {
+      const int cg = pi & 3, pxi = pi >> 2;
+      const int prl = pxi / pl.wo, pc = pxi - prl * pl.wo;
+      const int oy = q.pr0 + prl, cb = 16 * cg;
+      const uint4 dm = *reinterpret_cast<const uint4*>(s_dir + cb);
+      uint4 best = make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int ch = cb + 4 * s4;
-        *reinterpret_cast<uint32_t*>(pl.out_code + btile_off((int)(m >> 5), ch >> 5, ct, (int)(m & 31) + 32 * ((ch >> 2) & 1)) +
-                                     4 * ((ch & 31) >> 3)) = qd[s4];
-      }
-    }
+      for (int r = 0; r < 3; ++r) {
+        const int sy = 2 * oy - 1 + r;
 #pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      const qnn_code_out& co = o ? pl.c1 : pl.c0;
-      if (!co.ptr) continue;
-      const int8_t* sl = smem + (o ? pl.lds_lut1 : pl.lds_lut0);
-      int r4[4];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        r4[s4] = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int ch = cb + 4 * s4 + u;
-          r4[s4] |= ((int)(uint8_t)sl[ch * 256 + ((qd[s4] >> (8 * u)) & 255)]) << (8 * u);
+        for (int s2 = 0; s2 < 3; ++s2) {
+          const int sx = 2 * pc - 1 + s2;
+          // MaxPool2d pads with -inf: an out-of-image tap reads a clamped pixel and is masked
+          // to 0, the identity of the folded-code max
+          const bool okt = sy >= 0 && sy < d.ho && sx >= 0 && sx < d.wo;
+          const int ly = min(max(sy, q.sr_lo), q.sr_hi) - q.sr_lo, lx = min(max(sx, 0), d.wo - 1);
+          const uint4 v = *reinterpret_cast<const uint4*>(s_codes + (ly * d.wo + lx) * C + cb);
+          const uint32_t msk = okt ? 0xffffffffu : 0u;
+          best.x = max_u8x4(best.x, (v.x ^ dm.x) & msk);
+          best.y = max_u8x4(best.y, (v.y ^ dm.y) & msk);
+          best.z = max_u8x4(best.z, (v.z ^ dm.z) & msk);
+          best.w = max_u8x4(best.w, (v.w ^ dm.w) & msk);
         }
       }
-      *reinterpret_cast<int4*>(co.ptr + (((int64_t)img * co.hp + oy + co.pad) * co.wp + pc + co.pad) * co.cp + cb) =
-          make_int4(r4[0], r4[1], r4[2], r4[3]);
+      const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
+      const int64_t m = ((int64_t)q.img * pl.ho + oy) * pl.wo + pc;
+      if (pl.out_code) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int ch = cb + 4 * s4;
+          *reinterpret_cast<uint32_t*>(pl.out_code + btile_off((int)(m >> 5), ch >> 5, ct, (int)(m & 31) + 32 * ((ch >> 2) & 1)) +
+                                       4 * ((ch & 31) >> 3)) = qd[s4];
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        const qnn_code_out& co = o ? pl.c1 : pl.c0;
+        if (!co.ptr) continue;
+        const int8_t* sl = smem + (o ? pl.lds_lut1 : pl.lds_lut0);
+        int r4[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          r4[s4] = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int ch = cb + 4 * s4 + u;
+            r4[s4] |= ((int)(uint8_t)sl[ch * 256 + ((qd[s4] >> (8 * u)) & 255)]) << (8 * u);
+          }
+        }
+        *reinterpret_cast<int4*>(co.ptr + (((int64_t)q.img * co.hp + oy + co.pad) * co.wp + pc + co.pad) * co.cp + cb) =
+            make_int4(r4[0], r4[1], r4[2], r4[3]);
+      }
     }
   }
 }
@@ -273,12 +304,16 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool&
   off += pl.lut1 ? 256 * C : 0;
   pl.lds_zero = off;
   off += 16;
-  pl.lds_band = off;  // (2 PR + 1) stem rows read (2 PR) * sh + kh padded input rows, 1 KiB DMA pieces
-  off += (int)cdiv((int64_t)(2 * PR * p.d.sh + p.d.kh) * p.d.wp * p.d.cp, 1024) * 1024;
+  pl.lds_band = off;  // two bands: (2 PR + 1) stem rows read (2 PR) * sh + kh padded input rows, 1 KiB pieces
+  pl.lds_band_bytes = (int)cdiv((int64_t)(2 * PR * p.d.sh + p.d.kh) * p.d.wp * p.d.cp, 1024) * 1024;
+  off += 2 * pl.lds_band_bytes;
   pl.lds_codes = off;
   off += (2 * PR + 1) * p.d.wo * C;
   if (off > LDS_MAX) return arg_error("stem max-pool tile needs more than 160 KiB of LDS");
-  const int nblk = p.d.n * pl.nrg;
+  pl.nitems = p.d.n * pl.nrg;
+  int per_cu = 0;  // persistent: as many blocks as fit at once, each walking the items
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, off) != hipSuccess || per_cu < 1) per_cu = 1;
+  const int nblk = (int)std::min<int64_t>(pl.nitems, (int64_t)device_cu_count() * per_cu);
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(NT), off, s, x, w, p, pl);
   return QNN_OK;
 }

@@ -99,6 +99,31 @@ def allreduce_calibration(model, group=None, samples=1):
             off += n
 
 
+def build_engine(model, batch, group=None, **kw):
+    """A qnn.Engine for this rank whose tile configurations are rank 0's: rank 0 autotunes
+    (times every configuration on its device) and broadcasts its choice, the other ranks plan
+    with it instead of timing their own -- so every rank of a data-parallel job runs the same
+    kernels (no per-rank timing skew in a max-over-ranks measurement; bitwise the same either
+    way, every configuration computes identical outputs).  World size 1: a plain Engine."""
+    from .engine import Engine
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return Engine(model, batch, **kw)
+    rank = dist.get_rank(group)
+    eng = Engine(model, batch, **kw) if rank == 0 else None
+    n = torch.tensor([len(eng.tiles) if eng is not None else 0], dtype=torch.int64)
+    dev_comm = dist.get_backend(group) == "nccl"
+    if dev_comm:
+        n = n.cuda()
+    dist.broadcast(n, 0, group=group)
+    t = torch.tensor([k for k, _ in eng.tiles] if eng is not None else [0] * int(n.item()), dtype=torch.int64)
+    if dev_comm:
+        t = t.cuda()
+    dist.broadcast(t, 0, group=group)
+    if eng is None:
+        eng = Engine(model, batch, tiles=[int(v) for v in t.cpu().tolist()], **kw)
+    return eng
+
+
 class _Pending:
     """An in-flight gather (ShardedInference.submit): result() waits and returns the
     [global_batch, ...] logits on root, None elsewhere."""

@@ -74,14 +74,17 @@ class Engine:
     nothing) avoids the copy.  graph=False runs the launches eagerly (debugging)."""
 
     def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None, fuse_stem_pool=True,
-                 max_links=None):
+                 max_links=None, tiles=None):
         """tile=k forces tile configuration k on every contraction it is built for (the
         others keep the cost model's choice); tile=None autotunes (or the cost model
         when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile.
         fuse_stem_pool: the ResNet stem conv and its max-pool as one launch
         (qnn_qconv2d_maxpool_fwd) where the shapes allow; False keeps two launches.
         max_links: the longest residual code chain (0 .. QNN_MAX_RES; 0 = every block
-        output an fp32 map); None = QNN_ENGINE_MAX_LINKS or QNN_MAX_RES."""
+        output an fp32 map); None = QNN_ENGINE_MAX_LINKS or QNN_MAX_RES.
+        tiles: an explicit configuration per contraction (e.g. another rank's autotuned
+        `engine.tiles`, qnn.dist.build_engine); one not built for this plan falls back to
+        the cost model's choice."""
         self.fuse_stem_pool = fuse_stem_pool
         if max_links is None:
             max_links = int(os.environ.get("QNN_ENGINE_MAX_LINKS", _lib.MAX_RES))
@@ -120,6 +123,16 @@ class Engine:
             for (_i, d, _e), k in zip(self.convs, ks):
                 d.tile = k + 1
             self.tiles = [(k, None) for k in ks]
+        elif tiles is not None:
+            if len(tiles) != len(self.convs):
+                raise ValueError(f"qnn.Engine: {len(tiles)} tiles for a plan of {len(self.convs)} convs")
+            self.tiles, self.tiles_fallback = [], []
+            for n, ((_i, d, e), k) in enumerate(zip(self.convs, tiles)):
+                d.tile = int(k) + 1
+                if not self._plan_ok(d, e):
+                    d.tile = 0
+                    self.tiles_fallback.append(n)
+                self.tiles.append((self.plan(d, e)[0], None))
         elif tile is not None:
             self.tiles = []
             for _i, d, e in self.convs:

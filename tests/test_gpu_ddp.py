@@ -150,8 +150,7 @@ def _eval_worker(rank, world, port, out):
     from conftest import load_fixture
     from fixtures_util import build_model
     from qnn import synthetic
-    from qnn.dist import ShardedInference, allreduce_calibration, shard_bounds
-    from qnn.engine import Engine
+    from qnn.dist import ShardedInference, allreduce_calibration, build_engine, shard_bounds
     dev = torch.device("cuda:0")
     model, _ = build_model(load_fixture(FIXTURE))
     model = model.to(dev)
@@ -159,7 +158,8 @@ def _eval_worker(rank, world, port, out):
     _calibrate(model, batches, dev)
     allreduce_calibration(model, samples=batches[0].shape[0])
     s, e = shard_bounds(GB_EVAL, world, rank)
-    eng = Engine(model, batch=e - s)
+    eng = build_engine(model, e - s)  # rank 0 autotunes, rank 1 runs its tiles
+    torch.save(([k for k, _ in eng.tiles], getattr(eng, "tiles_fallback", [])), f"{out}.tiles{rank}")
     runner = ShardedInference(eng, GB_EVAL)
     x = synthetic.input_batch((GB_EVAL, 3, 32, 32), 600).to(dev)
     logits = runner(x[s:e])
@@ -181,6 +181,9 @@ def test_sharded_engine_world2_device(gpu, tmp_path):
     out = str(tmp_path / "eval.pt")
     _spawn(_eval_worker, (out,))
     got = torch.load(out, weights_only=True)
+    (t0, _), (t1, fb1) = [torch.load(f"{out}.tiles{r}", weights_only=True) for r in range(2)]
+    # rank 1 runs rank 0's configuration wherever it is built for rank 1's (ragged) shard
+    assert all(a == b for n, (a, b) in enumerate(zip(t0, t1)) if n not in fb1), (t0, t1, fb1)
     # single process: each shard's calibration on its own, merged with the sample weights
     states = []
     for r in range(2):

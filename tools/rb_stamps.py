@@ -75,9 +75,9 @@ def report(tag, us, nblk, w):
             cum = np.cumsum(c.mean((0, 1)))
             print(f"   team {tm}: " + "  ".join(f"{a}={m:.0f}" for a, m in zip(names, c.mean((0, 1)))) +
                   "   cumulative end of each phase: " + " ".join(f"{x:.0f}" for x in cum))
-        pro = w[:, 4:8, 8:15].mean((0, 1))
-        print("   team 1 prologue (cycles from start): issued {:.0f}, chunks landed {:.0f} {:.0f} {:.0f} {:.0f}, "
-              "pixel sums {:.0f}, epilogue data staged {:.0f}".format(*pro))
+        pro = w[:, :, 8:12].mean((0, 1))
+        print("   prologue (cycles from start, all waves): barrier passed {:.0f}, chunk 0 + weights issued {:.0f}, "
+              "own pieces landed {:.0f}, summed {:.0f}".format(*pro))
     rs = w[:, 0, 0] - w[:, 0, 0].min()
     re_ = w[:, 0, 1] - w[:, 0, 0].min()
     life = re_ - rs
