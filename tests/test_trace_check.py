@@ -1,0 +1,68 @@
+"""tools/trace_check.py (CPU): finds bench.py's timed graph replays in a rocprofv3 kernel trace,
+recomputes the roofline fraction from the trace, and refuses a trace that does not describe the
+benched build (per-forward kernel sum above ms_per_step) or a frac off by more than 5 %."""
+import csv
+import json
+import os
+import sys
+
+from conftest import REPO
+
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+NAMES = ["void qnn::quantize_s2d_x2_kernel<1, 3>(int)", "void qnn::sp::stem_pool_kernel<4, true>(int)",
+         "void qnn::qconv_kernel<qnn::Cfg<1>>(int)", "void qnn::avgpool_quant_kernel(int)"]
+DUR = [20_000, 100_000, 50_000, 5_000]  # ns
+
+
+def _write(tmp, steps=20, warmup=5, conv_frac=None, ms_per_step=None):
+    rows, t = [], 1_000_000
+    def emit(name, dur):
+        nonlocal t
+        rows.append({"Kernel_Name": name, "Start_Timestamp": t, "End_Timestamp": t + dur})
+        t += dur + 1_000
+    for _ in range(3):  # autotune: one conv repeated
+        emit(NAMES[2], 60_000)
+    for _ in range(1 + warmup + steps):  # capture warm-up + the replays
+        for n, dur in zip(NAMES, DUR):
+            emit(n, dur)
+        emit("void at::native::copy_kernel(int)", 2_000)  # torch copies are not qnn launches
+    for _ in range(steps):  # the conv-only timing graph (period 2)
+        emit(NAMES[1], 100_000)
+        emit(NAMES[2], 50_000)
+    trace = os.path.join(tmp, "run_kernel_trace.csv")
+    with open(trace, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        w.writerows(rows)
+    conv_ms = 0.152  # in-graph conv time incl. launch gaps (> the 0.150 of kernel time)
+    ops = 1e12 * 0.75
+    achieved = ops / (conv_ms * 1e-3) / 1e12
+    frac = conv_frac if conv_frac is not None else achieved / 5000.0
+    line = {"steps": steps, "ms_per_step": ms_per_step or 0.2,
+            "engine": {"launches_per_forward": 4},
+            "roofline": {"achieved": achieved, "frac": frac, "kernel_ms_per_forward": conv_ms}}
+    bj = os.path.join(tmp, "bench.json")
+    with open(bj, "w") as f:
+        f.write("some log line\n" + json.dumps(line) + "\n")
+    return trace, bj
+
+
+def test_trace_check_accepts_consistent_trace(tmp_path):
+    import trace_check
+    trace, bj = _write(str(tmp_path))
+    out = str(tmp_path / "out.json")
+    assert trace_check.main(trace, bj, out) == 0
+    r = json.load(open(out))
+    assert abs(r["trace_kernel_ms_per_forward"] - 0.175) < 1e-9
+    assert abs(r["trace_conv_ms_per_forward"] - 0.150) < 1e-9
+    assert r["checks"] == {"trace_sum_le_ms_per_step": True, "frac_within_5pct": True}
+    assert [x["us"] for x in r["launches"]] == [20.0, 100.0, 50.0, 5.0]
+
+
+def test_trace_check_refuses_stale_trace(tmp_path):
+    import trace_check
+    trace, bj = _write(str(tmp_path), ms_per_step=0.17)  # kernels alone take 0.175 ms
+    assert trace_check.main(trace, bj, str(tmp_path / "o.json")) == 1
+    trace, bj = _write(str(tmp_path), conv_frac=0.2)  # the bench's frac disagrees with the trace
+    assert trace_check.main(trace, bj, str(tmp_path / "o2.json")) == 1

@@ -7,6 +7,7 @@
 #   bench[:ARGS]       python bench.py ARGS  (ARGS: comma-separated, e.g. bench:--depth,50,--batch,256)
 #   prof:MODEL:DEPTH:BATCH   tools/gpu_prof.sh (kernel trace of 10 graph replays + PMC traffic)
 #   benchprof[:ARGS]   rocprofv3 --kernel-trace --stats of the bench command itself
+#   tracecheck[:ARGS]  tools/trace_check.py on that trace and bench line (same ARGS)
 #   pmc:MODEL:DEPTH:BATCH:C1,C2,..  one rocprofv3 --pmc pass (eager launches) + tools/pmc_table.py
 #   py:SCRIPT[:ARGS]   python SCRIPT ARGS (comma-separated)
 # Every step runs under its own timeout; the first failing step ends the run.
@@ -43,6 +44,9 @@ for S in "$@"; do
            python3 tools/layer_table.py run --model $M --depth $D --batch $B --fwd 2 --eager --meta $P/meta.json > $P/run.log 2>&1
          rc=$?; [ $rc -eq 0 ] && python3 tools/pmc_table.py $P/meta.json $P/raw --json $P/pmc.json > $P/pmc.txt 2>&1; rc=$?
          cat $P/pmc.txt | head -70 ;;
+    tracecheck) N=$(echo "$ARGS" | tr -d ' -' | head -c 40)
+           T=$(ls $O/benchprof_$N/*/run_kernel_trace.csv $O/benchprof_$N/run_kernel_trace.csv 2>/dev/null | head -1)
+           python3 tools/trace_check.py $T $O/benchprof_$N.json $O/tracecheck_$N.json; rc=$? ;;
     py) SCR=${ARG%%:*}; PA=${ARG#*:}; [ "$PA" = "$ARG" ] && PA=""; PA=${PA//,/ }
         N=$(basename $SCR .py)
         timeout -k 10 600 python -u $SCR $PA > $O/$N.out 2> $O/$N.err
