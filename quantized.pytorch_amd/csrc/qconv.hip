@@ -1451,12 +1451,14 @@ static const CfgInfo CFG[NCFG] = {
 };
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
-static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count(); }
+static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count(); }
 static int rb_first() { return NCFG + q16_count(); }
 static int rbp_first() { return NCFG + q16_count() + rb_count(); }
+static int dtab_first() { return rbp_first() + rbp_count(); }
 
 static bool cfg_ok(int k, const Params& p) {
   if (k >= ncfg_all()) return false;
+  if (k >= dtab_first()) return dtab_ok(k - dtab_first(), p);
   if (k >= rbp_first()) return rbp_ok(k - rbp_first(), p);
   if (k >= rb_first()) return rb_ok(k - rb_first(), p);
   if (k >= NCFG) return q16_ok(k - NCFG, p);
@@ -1473,6 +1475,7 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
+  if (k >= dtab_first()) return dtab_cost(k - dtab_first(), p);
   if (k >= rbp_first()) return rbp_cost(k - rbp_first(), p);
   if (k >= rb_first()) return rb_cost(k - rb_first(), p);
   if (k >= NCFG) return q16_cost(k - NCFG, p);
@@ -1506,6 +1509,7 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (k >= dtab_first()) return dtab_launch(k - dtab_first(), x, w, p, s);
   if (k >= rbp_first()) return rbp_launch(k - rbp_first(), x, w, p, s);
   if (k >= rb_first()) return rb_launch(k - rb_first(), x, w, p, s);
   if (k >= NCFG) return q16_launch(k - NCFG, x, w, p, s);
@@ -1585,6 +1589,7 @@ extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
 extern "C" const char* qnn_conv_tile_kernel(int k) {
   if (k < 0 || k >= ncfg_all()) return nullptr;
+  if (k >= dtab_first()) return "qconv_dtab_kernel";
   if (k >= rbp_first()) return "qconv_rbp_kernel";
   if (k >= rb_first()) return k - rb_first() < rb_count() - direct_count() ? "qconv_rb_kernel" : "qconv_direct_kernel";
   if (k >= NCFG) return "qconv16_kernel";
@@ -1603,14 +1608,16 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   int tbm, tbn;
-  if (k >= rbp_first()) rbp_tile(k - rbp_first(), &tbm, &tbn);
+  if (k >= dtab_first()) dtab_tile(k - dtab_first(), &tbm, &tbn);
+  else if (k >= rbp_first()) rbp_tile(k - rbp_first(), &tbm, &tbn);
   else if (k >= rb_first()) rb_tile(k - rb_first(), &tbm, &tbn);
   else if (k >= NCFG) q16_tile(k - NCFG, &tbm, &tbn);
   else tbm = CFG[k].bm, tbn = CFG[k].bn;
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
   if (nblk)
-    *nblk = k >= rbp_first() ? (int)rbp_blocks(k - rbp_first(), p)
+    *nblk = k >= dtab_first() ? (int)dtab_blocks(k - dtab_first(), p)
+            : k >= rbp_first() ? (int)rbp_blocks(k - rbp_first(), p)
             : k >= rb_first() ? (int)rb_blocks(k - rb_first(), p)
                               : (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm));
   return QNN_OK;
@@ -1658,8 +1665,9 @@ extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue*
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   QNN_REQUIRE(k >= rb_first(), "occupancy is reported for the resident-band and direct-fragment configurations");
   Occ o{0, 0, 0};
-  const int r = k >= rbp_first() ? rbp_launch(k - rbp_first(), nullptr, nullptr, p, nullptr, &o)
-                                 : rb_launch(k - rb_first(), nullptr, nullptr, p, nullptr, &o);
+  const int r = k >= dtab_first()  ? dtab_launch(k - dtab_first(), nullptr, nullptr, p, nullptr, &o)
+                : k >= rbp_first() ? rbp_launch(k - rbp_first(), nullptr, nullptr, p, nullptr, &o)
+                                   : rb_launch(k - rb_first(), nullptr, nullptr, p, nullptr, &o);
   if (r != QNN_OK) return r;
   if (cfg) *cfg = k;
   if (blocks_per_cu) *blocks_per_cu = o.blocks_per_cu;

@@ -95,12 +95,14 @@ def test_tile_kernel_families(lib):
     from qnn import _lib
     fams = [_lib.tile_kernel(k) for k in range(_lib.CONV_TILES)]
     assert set(fams) == {"qconv_kernel", "qconv_pp_kernel", "qconv_band_kernel", "qconv16_kernel",
-                         "qconv_rb_kernel", "qconv_direct_kernel", "qconv_rbp_kernel"}
-    # families are contiguous id ranges, the two-team resident band last (appended in round 4)
+                         "qconv_rb_kernel", "qconv_direct_kernel", "qconv_rbp_kernel", "qconv_dtab_kernel"}
+    # families are contiguous id ranges; round 4 appended the two-team resident band, then the
+    # table-epilogue direct configurations (ids of earlier families never move)
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
     assert len(runs) == len(set(runs)) + 1  # the ring family is split by the ping-pong ids 6-9
     assert len(_lib.tile_ids("qconv_direct_kernel")) == 5
-    assert fams[-1] == "qconv_rbp_kernel" and _lib.tile_ids("qconv_rbp_kernel") == [40, 41]
+    assert _lib.tile_ids("qconv_rbp_kernel") == [40, 41]
+    assert fams[-1] == "qconv_dtab_kernel" and _lib.tile_ids("qconv_dtab_kernel") == [42, 43]
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 
