@@ -411,8 +411,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void q
   // lane per output pixel sums its taps of the band-pixel sums (padding codes are 0, so this is
   // the receptive field's exact sum)
   if (team == 0) {
-    if (tw == 0 && lane < d.ho + d.wo)  // the border-class tables
-      s_hc[lane] = lane < d.ho ? e.hcls[lane] * e.nwc : e.wcls[lane - d.ho];
+    if (tw == 0)  // the border-class tables (ho + wo entries: more than one wave's lanes at 56x56)
+      for (int i = lane; i < d.ho + d.wo; i += 64) s_hc[i] = i < d.ho ? e.hcls[i] * e.nwc : e.wcls[i - d.ho];
     poll(&s_sync[20], 8);
     for (int q = 64 * tw + lane; q < C::BN; q += 256) {
       int qq = q < npx_blk ? q : npx_blk - 1;

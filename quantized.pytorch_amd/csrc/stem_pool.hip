@@ -46,13 +46,15 @@ struct Cfg {  // what stage_epi expects
 };
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t max_u8x4(uint32_t a, uint32_t b) {
-  u16x2 alo = __builtin_bit_cast(u16x2, a & 0x00ff00ffu), ahi = __builtin_bit_cast(u16x2, (a >> 8) & 0x00ff00ffu);
-  u16x2 blo = __builtin_bit_cast(u16x2, b & 0x00ff00ffu), bhi = __builtin_bit_cast(u16x2, (b >> 8) & 0x00ff00ffu);
-  u16x2 lo = __builtin_elementwise_max(alo, blo), hi = __builtin_elementwise_max(ahi, bhi);
-  return __builtin_bit_cast(uint32_t, lo) | (__builtin_bit_cast(uint32_t, hi) << 8);
-}
 
+// q = m / D, r = m % D for 0 <= m < 2^24: the float quotient is off by at most one, fixed up
+// exactly (qconv_direct.hip's fdivmod) -- a few VALU ops where an integer division costs ~40
+__device__ __forceinline__ void fdivmod(int m, int D, float invD, int& q, int& r) {
+  q = (int)((float)m * invD);
+  r = m - (int)__umul24((unsigned)q, (unsigned)D);
+  if (r < 0) --q, r += D;
+  if (r >= D) ++q, r -= D;
+}
 struct Pool {
   int ho, wo;            // pooled output
   int nrg;               // row groups per image (ceil(ho / PR))
@@ -151,9 +153,22 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
     bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * C + cl);
   }
   uint8_t* s_codes = reinterpret_cast<uint8_t*>(smem + pl.lds_codes);
-  // pool direction per channel: 0xff where relu o RangeBN is non-increasing (sq * wq < 0)
+  // pool direction per channel: 0xff where relu o RangeBN is non-increasing (sq * wq < 0).  The
+  // tiles store their codes XOR the direction (the pooling's folded form), so the window
+  // reduction is a plain bytewise max and only its result is unfolded.
   uint8_t* s_dir = reinterpret_cast<uint8_t*>(smem + pl.lds_dir);
   if (tid < C) s_dir[tid] = (s_f[4 * C + tid] * s_f[5 * C + tid]) < 0.f ? 0xff : 0;
+  uint32_t dirw[TM];  // this lane's four channels of each row tile
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    dirw[i] = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ch = 16 * i + 4 * g + u;
+      dirw[i] |= ((s_f[4 * C + ch] * s_f[5 * C + ch]) < 0.f ? 0xffu : 0u) << (8 * u);
+    }
+  }
+  const float inv_wo = 1.0f / (float)d.wo, inv_pwo = 1.0f / (float)pl.wo;
   const int ct = (C + 31) >> 5;
 
   for (int buf = 0; it < pl.nitems; it += gridDim.x, buf ^= 1) {
@@ -168,8 +183,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
     auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
       int qq = t * 16 + (lane & 15);
       qq = qq < q.npx ? qq : q.npx - 1;  // past the rows: the last pixel again (its store is skipped)
-      lr = qq / d.wo;
-      col = qq - lr * d.wo;
+      fdivmod(qq, d.wo, inv_wo, lr, col);
       const int base = band + (lr * d.sh * d.wp + col * d.sw) * d.cp;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -224,36 +238,49 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
                       (f2){bi[i].z, bi[i].w};
         const int kb = pack4(qclamp2(v0, bnp) + MAGIC_U8, qclamp2(v1, bnp) + MAGIC_U8);  // EK_BNCODE
-        if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb;
+        if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb ^ (int)dirw[i];
       }
     }
     __syncthreads();
 
-    // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest
+    // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest.  MaxPool2d pads with
+    //         -inf: an out-of-image tap is clamped to the nearest in-image row / column, which
+    //         lies inside the same window (2*oy and 2*pc are always in the image), and the max is
+    //         idempotent.  The folded bytes are reduced as even / odd halves in u16 lanes
+    //         (v_perm_b32 splits, v_pk_max_u16), rejoined once.
     for (int pi = tid; pi < q.npr * pl.wo * 4 && QNN_SP_ABLATE != 3; pi += NT) {
       const int cg = pi & 3, pxi = pi >> 2;
-      const int prl = pxi / pl.wo, pc = pxi - prl * pl.wo;
+      int prl, pc;
+      fdivmod(pxi, pl.wo, inv_pwo, prl, pc);
       const int oy = q.pr0 + prl, cb = 16 * cg;
       const uint4 dm = *reinterpret_cast<const uint4*>(s_dir + cb);
-      uint4 best = make_uint4(0, 0, 0, 0);
+      int roff[3], coff[3];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const int sy = 2 * oy - 1 + r;
+        const int sy = min(max(2 * oy - 1 + r, 0), d.ho - 1);
+        roff[r] = (min(max(sy, q.sr_lo), q.sr_hi) - q.sr_lo) * d.wo * C + cb;
+        coff[r] = min(max(2 * pc - 1 + r, 0), d.wo - 1) * C;
+      }
+      u16x2 lo[4], hi[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lo[k] = hi[k] = (u16x2){0, 0};
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int s2 = 0; s2 < 3; ++s2) {
-          const int sx = 2 * pc - 1 + s2;
-          // MaxPool2d pads with -inf: an out-of-image tap reads a clamped pixel and is masked
-          // to 0, the identity of the folded-code max
-          const bool okt = sy >= 0 && sy < d.ho && sx >= 0 && sx < d.wo;
-          const int ly = min(max(sy, q.sr_lo), q.sr_hi) - q.sr_lo, lx = min(max(sx, 0), d.wo - 1);
-          const uint4 v = *reinterpret_cast<const uint4*>(s_codes + (ly * d.wo + lx) * C + cb);
-          const uint32_t msk = okt ? 0xffffffffu : 0u;
-          best.x = max_u8x4(best.x, (v.x ^ dm.x) & msk);
-          best.y = max_u8x4(best.y, (v.y ^ dm.y) & msk);
-          best.z = max_u8x4(best.z, (v.z ^ dm.z) & msk);
-          best.w = max_u8x4(best.w, (v.w ^ dm.w) & msk);
+          const uint4 v = *reinterpret_cast<const uint4*>(s_codes + roff[r] + coff[s2]);
+          const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            lo[k] = __builtin_elementwise_max(lo[k], __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, vv[k], 0x0c020c00u)));
+            hi[k] = __builtin_elementwise_max(hi[k], __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, vv[k], 0x0c030c01u)));
+          }
         }
-      }
+      uint4 best;
+      best.x = __builtin_bit_cast(uint32_t, lo[0]) | (__builtin_bit_cast(uint32_t, hi[0]) << 8);
+      best.y = __builtin_bit_cast(uint32_t, lo[1]) | (__builtin_bit_cast(uint32_t, hi[1]) << 8);
+      best.z = __builtin_bit_cast(uint32_t, lo[2]) | (__builtin_bit_cast(uint32_t, hi[2]) << 8);
+      best.w = __builtin_bit_cast(uint32_t, lo[3]) | (__builtin_bit_cast(uint32_t, hi[3]) << 8);
       const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
       const int64_t m = ((int64_t)q.img * pl.ho + oy) * pl.wo + pc;
       if (pl.out_code) {
