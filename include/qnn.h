@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 8
+#define QNN_ABI_VERSION 9
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -391,6 +391,16 @@ int qnn_dwconv_fused_generic(const int8_t* x, int n, int h, int w, int pad, int 
                              const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
                              float x_scale, const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
                              const qnn_code_out* code0, qnn_stream_t stream);
+
+/* qnn_dwconv_fused with RangeBN -> ReLU -> the consumer's quantizer looked up instead of
+ * evaluated: lut = qnn_bn_code_lut(bn, c, relu, code0) ([c][256] over the RangeBN input code,
+ * bitwise the evaluated chain), codes out only, 3x3 stride 1 or 2, c % 8 == 0 (and c % 128 == 0
+ * above 128 channels), lut 16-byte aligned; anything else is an argument error (round 4: the
+ * MobileNet engine's depthwise launches). */
+int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                         const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
+                         float x_scale, const float* bias, const qnn_bn_params* bn, const int8_t* lut,
+                         const qnn_code_out* code0, qnn_stream_t stream);
 
 /* nn.AvgPool2d(k) over the whole k x k map (resnet_quantized.py:153, mobilenet_quantized.py:157)
  * on fp32 x [n*hw][c] (NHWC, or the C-tile layout when x_tiled): mean = (sum in row-major

@@ -9,9 +9,6 @@
 
 #include "qconv_common.h"
 
-#ifndef QNN_DW_PF
-#define QNN_DW_PF 1  // depthwise: 1 = next group's loads in flight under this one (register double buffer)
-#endif
 #ifndef QNN_DW_WPE
 #define QNN_DW_WPE 2  // depthwise: waves per SIMD the register budget is sized for
 #endif
@@ -220,23 +217,29 @@ __global__ void dwconv_fused_kernel(const int8_t* __restrict__ x, int n, int h, 
 // x_hat = fl(fl(q*s)+min), fmaf into the accumulator in (r, s) row-major order with
 // out-of-image taps skipped, + bias, RangeBN on its quantized input, ReLU, the
 // consumer's codes.  Layout of the work instead: a thread owns 8 channels (8-byte
-// loads, coalesced along channels across the ct = c/8 channel threads) of R
+// loads, coalesced along channels across the ct = cs/8 channel threads) of R
 // consecutive output pixels of one row, so each input column is dequantized once
 // and feeds up to 3 outputs from registers; the 9x8 tap weights, the bias and the
 // RangeBN vectors live in registers; both quantizers run division-free
 // (quant_code_fast, bit-identical); no 64-bit index arithmetic.
-template <int S, int R, int P>
+// LUT (qnn_dwconv_fused_lut): RangeBN -> ReLU -> the consumer's quantizer of each channel is
+// the exact per-channel table qnn_bn_code_lut builds over the RangeBN input code (the conv
+// kernels' EK_LUT), so after the RangeBN input quotient each code is one LDS byte lookup --
+// half the kernel's VALU work per output was that chain.  A block then covers a slice of cs
+// channels (<= 128: a 32 KiB table slice in LDS), blocks of one pixel range and every slice
+// adjacent in the XCD-grouped order.
+template <int S, int R, int P, bool LUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE))) void dwconv3_kernel(const int8_t* __restrict__ x, int h, int w, int pad, int hp,
                                                       int wp, int cp, int c, const float* __restrict__ wt, int ho,
                                                       int wo, float x_min, float x_scale, const float* bias,
-                                                      qnn_bn_params bn, float bn_inv, int has_bn, int relu,
-                                                      float* out_f32, qnn_code_out c0, float c0_inv, int rows) {
+                                                      qnn_bn_params bn, int has_bn, int relu,
+                                                      float* out_f32, qnn_code_out c0, int rows, const int8_t* __restrict__ lut,
+                                                      int cs) {
   constexpr int K = 3, NCOL = (R - 1) * S + K, CPT = 2 * P;  // CPT channels per thread
   using LT = std::conditional_t<P == 4, uint2, uint32_t>;    // one tap of them: 8 or 4 code bytes
-  const int ct = c / CPT, per_blk = 256 / ct;
+  const int nsl = c / cs, ct = cs / CPT, per_blk = 256 / ct;
   const int tc = threadIdx.x % ct, tp = threadIdx.x / ct;
-  if (tp >= per_blk) return;  // c/CPT not a divisor of 256: idle tail threads
-  const int nxg = (wo + R - 1) / R, total = rows * nxg, cb = CPT * tc;
+  const int nxg = (wo + R - 1) / R, total = rows * nxg;
   // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
   // one), so logical block L = the bijective XCD-major index of b gives each XCD a contiguous
   // range of L -- adjacent output rows, whose 3x3 windows share input rows, are then computed
@@ -246,7 +249,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
     const int nb = gridDim.x, bb = blockIdx.x, xcd = bb & 7, q = nb >> 3, r = nb & 7;
     blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bb >> 3);
   }
-  if (blk * per_blk + tp >= total) return;
+  const int sl = blk % nsl, pblk = blk / nsl;   // channel slice, pixel block
+  const int cbl = CPT * tc, cb = sl * cs + cbl;  // this thread's channels: local, global
+  extern __shared__ __attribute__((aligned(16))) int8_t s_lut[];
+  if constexpr (LUT) {  // the slice's code table [cs][256], before any thread may leave
+    const int8_t* src = lut + (size_t)sl * cs * 256;
+    for (int i = 16 * threadIdx.x; i < cs * 256; i += 16 * 256)
+      *reinterpret_cast<uint4*>(s_lut + i) = *reinterpret_cast<const uint4*>(src + i);
+    __syncthreads();
+  }
+  if (tp >= per_blk) return;  // cs/CPT not a divisor of 256: idle tail threads
+  if (pblk * per_blk + tp >= total) return;
   // every per-channel quantity as packed pairs (channels 2p, 2p+1): v_pk_fma/mul/add run the
   // same IEEE fp32 op per element as the scalar form, so the results are bitwise unchanged
   f2 wv[K * K][P];
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     bi[p] = bias ? (f2){bias[cb + 2 * p], bias[cb + 2 * p + 1]} : (f2){0.f, 0.f};
-    if (has_bn) {
+    if (has_bn && !LUT) {
       mean[p] = (f2){bn.mean[cb + 2 * p], bn.mean[cb + 2 * p + 1]};
       sq[p] = (f2){bn.sq[cb + 2 * p], bn.sq[cb + 2 * p + 1]};
       wq[p] = (f2){bn.wq[cb + 2 * p], bn.wq[cb + 2 * p + 1]};
@@ -274,35 +287,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   const QParams c0p = make_qparams(c0.neg_min, c0.scale, c0.qmax);
   const f2 xs2 = {x_scale, x_scale}, xm2 = {x_min, x_min};
   const f2 bs2 = {bn.scale, bn.scale}, bm2 = {bn.min, bn.min};
-  (void)bn_inv, (void)c0_inv;
+  // (row, pixel group) of group g: float reciprocals with an exact fix-up (groups < 2^24 on
+  // the host), integer division otherwise
+  const bool fdiv = total < (1 << 24);
+  const float inv_nxg = 1.0f / (float)nxg, inv_ho = 1.0f / (float)ho;
+  auto divmod = [&](int m, int D, float invD, int& q, int& r) __attribute__((always_inline)) {
+    if (fdiv) {
+      q = (int)((float)m * invD);
+      r = m - (int)__umul24((unsigned)q, (unsigned)D);
+      if (r < 0) --q, r += D;
+      if (r >= D) ++q, r -= D;
+    } else {
+      q = m / D, r = m - q * D;
+    }
+  };
   // Every load unconditional (clamped in-buffer addresses: the padded buffer holds any row
   // oy*S + r and column < wp) and all K x NCOL issued together -- a load under a branch
   // gets its own vmcnt(0) wait.  Software-pipelined: the next group's loads are in flight
   // while this group computes.
-  auto load = [&](int g, LT (&v)[K][NCOL]) {
-    const int row = g / nxg, xg = g - row * nxg;
-    const int img = row / ho, oy = row - img * ho;
-    const int8_t* xrow = x + ((size_t)img * hp + oy * S) * wp * cp + cb;
+  // in-image offsets in 32 bits (a padded image is < 2^31 bytes on the host), one 64-bit base
+  const int wpcp = wp * cp;
+  auto load = [&](int g, LT (&v)[K][NCOL]) __attribute__((always_inline)) {
+    int row, xg, img, oy;
+    divmod(g, nxg, inv_nxg, row, xg);
+    divmod(row, ho, inv_ho, img, oy);
+    const int8_t* xrow = x + (size_t)(img * hp + oy * S) * (size_t)wpcp + cb;
 #pragma unroll
     for (int r = 0; r < K; ++r)
 #pragma unroll
       for (int col = 0; col < NCOL; ++col) {
         const int px = min(xg * R * S + col, wp - 1);
-        v[r][col] = *reinterpret_cast<const LT*>(xrow + ((size_t)r * wp + px) * cp);
+        v[r][col] = *reinterpret_cast<const LT*>(xrow + (r * wpcp + (int)__umul24((unsigned)px, (unsigned)cp)));
       }
   };
   // grid-stride over (row, R-pixel group): the register-resident parameters are loaded
   // once per thread and reused across all of its groups
-  const int step = gridDim.x * per_blk;
-  LT v[K][NCOL];
-  if (QNN_DW_PF) load(blk * per_blk + tp, v);
-  for (int pg = blk * per_blk + tp; pg < total; pg += step) {
-    const int row = pg / nxg, xg = pg - row * nxg;
-    const int img = row / ho, oy = row - img * ho;
+  const int step = (gridDim.x / nsl) * per_blk;
+  // one pixel group on operands v, the next group's loads into vn (two groups per trip, the
+  // buffers alternating: no register copies)
+  auto group = [&](int pg, LT (&v)[K][NCOL], LT (&vn)[K][NCOL]) __attribute__((always_inline)) {
+    int row, xg, img, oy;
+    divmod(pg, nxg, inv_nxg, row, xg);
+    divmod(row, ho, inv_ho, img, oy);
     const int ox0 = xg * R;
-    LT vn[K][NCOL];
-    if (QNN_DW_PF) load(min(pg + step, total - 1), vn);
-    else load(pg, v);
+    load(min(pg + step, total - 1), vn);
     f2 acc[R][P];
 #pragma unroll
     for (int j = 0; j < R; ++j)
@@ -342,6 +370,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
     for (int j = 0; j < R; ++j) {
       const int ox = ox0 + j;
       if (ox >= wo) break;
+      if constexpr (LUT) {
+        // RangeBN's input code per channel (the low mantissa byte of the magic-shifted clamped
+        // quotient = its rint), then the consumer's code from the slice's table
+        uint32_t cw[P / 2 > 0 ? P / 2 : 1];
+#pragma unroll
+        for (int p2 = 0; p2 < P; p2 += 2) {
+          uint32_t wd = 0;
+#pragma unroll
+          for (int p = p2; p < p2 + 2 && p < P; ++p) {
+            const f2 y = bias ? acc[j][p] + bi[p] : acc[j][p];
+            const f2 m = qclamp2(y, bnp) + MAGIC_U8;
+            const int ch = cbl + 2 * p;
+            const uint32_t b0 = (uint8_t)s_lut[ch * 256 + (__float_as_uint(m.x) & 255u)];
+            const uint32_t b1 = (uint8_t)s_lut[(ch + 1) * 256 + (__float_as_uint(m.y) & 255u)];
+            wd |= (b0 | (b1 << 8)) << (16 * (p - p2));
+          }
+          cw[p2 / 2] = wd;
+        }
+        int8_t* cp0 = c0.ptr + (size_t)((img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * (size_t)c0.cp + cb;
+        if constexpr (P == 4) *reinterpret_cast<uint2*>(cp0) = make_uint2(cw[0], cw[1]);
+        else *reinterpret_cast<uint32_t*>(cp0) = cw[0];
+        continue;
+      }
       f2 val[P];
 #pragma unroll
       for (int p = 0; p < P; ++p) {
@@ -363,7 +414,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
         if constexpr (P == 4) *reinterpret_cast<float4*>(o + 4) = make_float4(val[2].x, val[2].y, val[3].x, val[3].y);
       }
       if (c0.ptr) {
-        int8_t* cp0 = c0.ptr + (((size_t)img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * c0.cp + cb;
+        int8_t* cp0 = c0.ptr + (size_t)((img * c0.hp + oy + c0.pad) * c0.wp + ox + c0.pad) * (size_t)c0.cp + cb;
         const int p0 = pack4(qclamp2(val[0], c0p) + MAGIC_S8, qclamp2(val[1], c0p) + MAGIC_S8);
         if constexpr (P == 4) {
           const int p1 = pack4(qclamp2(val[2], c0p) + MAGIC_S8, qclamp2(val[3], c0p) + MAGIC_S8);
@@ -373,12 +424,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
         }
       }
     }
-    if (QNN_DW_PF) {
-#pragma unroll
-      for (int r = 0; r < K; ++r)
-#pragma unroll
-        for (int col = 0; col < NCOL; ++col) v[r][col] = vn[r][col];
-    }
+  };
+  LT va[K][NCOL], vb[K][NCOL];
+  load(pblk * per_blk + tp, va);
+  for (int pg = pblk * per_blk + tp; pg < total;) {
+    group(pg, va, vb);
+    pg += step;
+    if (pg >= total) break;
+    group(pg, vb, va);
+    pg += step;
   }
 }
 
@@ -494,7 +548,7 @@ int qnn_maxpool_bn(const uint8_t* q, int n, int h, int w, int c, int k, int stri
 static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
                         const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
                         float x_scale, const float* bias, const qnn_bn_params* bn, int relu, float* out_f32,
-                        const qnn_code_out* code0, qnn_stream_t stream, bool generic) {
+                        const qnn_code_out* code0, qnn_stream_t stream, bool generic, const int8_t* lut = nullptr) {
   QNN_REQUIRE(n >= 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && cp >= c && cp % 4 == 0 && kh > 0 && kw > 0 &&
                   sh > 0 && sw > 0 && pad >= 0,
               "bad shape");
@@ -514,21 +568,31 @@ static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, i
   const bool fast = !generic && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) && c % CPT == 0 &&
                     c / CPT <= 256 && cp % 8 == 0 && (((uintptr_t)x) & 7) == 0 && (((uintptr_t)w_hat_t) & 15) == 0 &&
                     (!out_f32 || (((uintptr_t)out_f32) & 15) == 0) &&
-                    (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0));
+                    (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0 &&
+                                 (int64_t)n * c0.hp * c0.wp < (1LL << 31))) &&  // 32-bit pixel indices
+                    (int64_t)n * hp < (1LL << 31) && 3LL * wp * cp < (1LL << 31);
+  // the table path: codes only, channel slices of 128 (or all c) channels
+  const int cs = lut ? (c > 128 ? 128 : c) : c;
+  const bool fast_lut = fast && lut && !out_f32 && c % cs == 0 && (((uintptr_t)lut) & 15) == 0;
+  if (lut && !fast_lut) return arg_error("qnn_dwconv_fused_lut: a 3x3 stride-1/2 layer with codes out only, c % 8 == 0 "
+                                        "(and c % 128 == 0 above 128 channels), 16-byte aligned table");
   if (fast) {
     const int R = sh == 1 ? 4 : 2;  // stride 2: 2 pixels (5 input columns) per thread, register budget
-    const int rows = n * ho, ct = c / CPT;
+    const int rows = n * ho, ct = cs / CPT, nsl = c / cs;
     const int64_t groups = (int64_t)rows * ((wo + R - 1) / R);
     QNN_REQUIRE(groups < (1LL << 31) && (int64_t)n * hp * wp * cp < (1LL << 40), "depthwise too large");
-    auto kern = sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P> : dwconv3_kernel<2, 2, QNN_DW_P>;
-    // grid-stride, sized to the resident capacity (the loop is software-pipelined)
+    auto kern = fast_lut ? (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, true> : dwconv3_kernel<2, 2, QNN_DW_P, true>)
+                         : (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, false> : dwconv3_kernel<2, 2, QNN_DW_P, false>);
+    const int lds = fast_lut ? cs * 256 : 0;
+    // grid-stride, sized to the resident capacity (the loop is software-pipelined); a whole
+    // number of channel slices per pixel block
     const int num_cu = device_cu_count();
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    const int blocks = (int)std::min<int64_t>(cdiv(groups, 256 / ct), (int64_t)num_cu * per_cu);
-    const float bn_inv = bn ? 1.0f / b.scale : 1.0f, c0_inv = c0.ptr ? 1.0f / c0.scale : 1.0f;
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, h, w, pad, hp, wp, cp, c, w_hat_t,
-                       ho, wo, x_min, x_scale, bias, b, bn_inv, bn ? 1 : 0, relu, out_f32, c0, c0_inv, rows);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int64_t pblocks = std::min<int64_t>(cdiv(groups, 256 / ct), std::max<int64_t>(1, (int64_t)num_cu * per_cu / nsl));
+    const int blocks = (int)(pblocks * nsl);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, (hipStream_t)stream, x, h, w, pad, hp, wp, cp, c, w_hat_t,
+                       ho, wo, x_min, x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0, rows, lut, cs);
     QNN_LAUNCH_CHECK("qnn_dwconv_fused");
     return QNN_OK;
   }
@@ -555,6 +619,15 @@ int qnn_dwconv_fused_generic(const int8_t* x, int n, int h, int w, int pad, int 
                              const qnn_code_out* code0, qnn_stream_t stream) {
   return dwconv_fused(x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min, x_scale, bias, bn, relu,
                       out_f32, code0, stream, true);
+}
+
+int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,
+                         const float* w_hat_t, int kh, int kw, int sh, int sw, int ho, int wo, float x_min,
+                         float x_scale, const float* bias, const qnn_bn_params* bn, const int8_t* lut,
+                         const qnn_code_out* code0, qnn_stream_t stream) {
+  QNN_REQUIRE(bn && lut && code0 && code0->ptr, "qnn_dwconv_fused_lut: RangeBN, its code table and a code output");
+  return dwconv_fused(x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min, x_scale, bias, bn, 1,
+                      nullptr, code0, stream, false, lut);
 }
 
 int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,

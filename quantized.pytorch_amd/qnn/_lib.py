@@ -16,7 +16,7 @@ import torch  # noqa: F401  (binds the process HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 CONV_TILES = 44  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
@@ -92,6 +92,8 @@ SIGNATURES = {
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused_generic": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
+    "qnn_dwconv_fused_lut": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_ptr, _PC, c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],
     "qnn_comm_unique_id": [c_ptr, ctypes.c_size_t],

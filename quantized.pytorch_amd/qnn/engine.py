@@ -590,10 +590,23 @@ class Engine:
             dargs = (N, x.H, x.W, p, xg["hp"], xg["wp"], xg["cp"], x.C)
             dargs2 = (k, k, st, st, Ho, Ho, float(dmn), x_scale)
             qb, xbp, wtp, br, pr = _lib.ptr(pk.qbias), _lib.ptr(xb), _lib.ptr(wt), ctypes.byref(b), ctypes.byref(pco)
-            self._add("qnn_dwconv_fused", lambda st, xbp=xbp, wtp=wtp, dargs=dargs, dargs2=dargs2, qb=qb, br=br, pr=pr:
-                      _lib.call("qnn_dwconv_fused", xbp, *dargs, wtp, *dargs2, qb, br, 1, None, pr, st),
-                      2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4,
-                      [N, Ho, Ho, x.C])
+            # RangeBN -> ReLU -> the pointwise quantizer as the exact per-channel code table (the
+            # conv epilogues' EK_LUT) where the 3x3 table kernel takes the layer, else evaluated
+            lut_ok = k == 3 and st in (1, 2) and x.C % 8 == 0 and (x.C <= 128 or x.C % 128 == 0)
+            if lut_ok:
+                lut = torch.empty((x.C, 256), dtype=torch.int8, device=self.dev)
+                _lib.call("qnn_bn_code_lut", br, x.C, 1, pr, _lib.ptr(lut), _lib.stream_of(lut))
+                self.keep.append(lut)
+                lp = _lib.ptr(lut)
+                self._add("qnn_dwconv_fused", lambda st, xbp=xbp, wtp=wtp, dargs=dargs, dargs2=dargs2, qb=qb, br=br,
+                          pr=pr, lp=lp: _lib.call("qnn_dwconv_fused_lut", xbp, *dargs, wtp, *dargs2, qb, br, lp, pr, st),
+                          2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4,
+                          [N, Ho, Ho, x.C])
+            else:
+                self._add("qnn_dwconv_fused", lambda st, xbp=xbp, wtp=wtp, dargs=dargs, dargs2=dargs2, qb=qb, br=br,
+                          pr=pr: _lib.call("qnn_dwconv_fused", xbp, *dargs, wtp, *dargs2, qb, br, 1, None, pr, st),
+                          2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4,
+                          [N, Ho, Ho, x.C])
             # pointwise + bn + relu -> next dw codes (or fp32 for the head)
             out = _Act(Ho, Ho, pw.out_channels)
             if last:

@@ -52,7 +52,7 @@ def test_bindings_cover_every_symbol(lib):
 
 def test_abi_version(lib):
     from qnn import _lib
-    assert lib.qnn_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.qnn_abi_version() == _lib.ABI_VERSION == 9
 
 
 def test_header_constants_match_bindings():

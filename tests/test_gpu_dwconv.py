@@ -85,3 +85,69 @@ def test_dwconv_fast_equals_generic_bitwise(gpu, n, h, c, s, with_bias, with_bn)
                                          groups=c).clamp_min(0).permute(0, 2, 3, 1)
         err = (f1.double() - ref).abs().max().item()
         assert err <= 1e-5 * ref.abs().max().item() + 1e-6, err
+
+
+@pytest.mark.parametrize("n,h,c,s,with_bias", [
+    (2, 14, 32, 1, True),
+    (3, 13, 64, 2, True),
+    (2, 7, 1024, 1, True),       # eight 128-channel slices
+    (4, 28, 256, 2, False),
+    (2, 56, 128, 1, True),
+    (1, 112, 32, 1, True),
+    (2, 29, 512, 2, True),       # odd extent, stride 2, four slices
+    (1, 15, 96, 1, False),       # one slice of 96 (c/8 = 12 does not divide 256)
+])
+def test_dwconv_lut_equals_evaluated_bitwise(gpu, n, h, c, s, with_bias):
+    """qnn_dwconv_fused_lut (RangeBN -> ReLU -> consumer quantizer looked up in the
+    qnn_bn_code_lut table, channel slices of <= 128 in LDS) writes bitwise the codes of the
+    evaluated chain (qnn_dwconv_fused), pad columns / rows of the consumer buffer untouched."""
+    g = torch.Generator().manual_seed(2000 + c + h)
+    k, pad = 3, 1
+    w = h
+    ho = (h + 2 * pad - k) // s + 1
+    wo = ho
+    cp = c
+    hp, wp = h + 2 * pad, w + 2 * pad
+    xc = torch.zeros((n, hp, wp, cp), dtype=torch.int8)
+    xc[:, pad:pad + h, pad:pad + w, :c] = torch.randint(-128, 128, (n, h, w, c), generator=g, dtype=torch.int8)
+    xmin, xs = -0.75, 3.1 / 255
+    wt = (torch.randn((k * k, c), generator=g) * 0.3).float().to(gpu)
+    bias = (torch.randn(c, generator=g) * 0.1).float().to(gpu) if with_bias else None
+    vecs = [torch.randn(c, generator=g) * 0.05, torch.rand(c, generator=g) + 0.5,
+            torch.rand(c, generator=g) * 2 - 0.5, torch.randn(c, generator=g) * 0.1]  # some wq < 0
+    vecs = [v.float().to(gpu) for v in vecs]
+    bn = _lib.BnParams(*[_lib.ptr(v) for v in vecs], 0.9, -0.9, 2.2 / 255, 255.0)
+    xg = xc.to(gpu)
+    st = _lib.stream_of(xg)
+    geom = (n, h, w, pad, hp, wp, cp, c, k, s, ho, wo, xmin, xs)
+    outs = []
+    for use_lut in (False, True):
+        oc = torch.full((n, ho + 2, wo + 2, cp), 77, dtype=torch.int8, device=gpu)
+        code = _lib.CodeOut(_lib.ptr(oc), cp, 1, ho + 2, wo + 2, 0.2, 1.7 / 255, 255.0)
+        if use_lut:
+            lut = torch.empty((c, 256), dtype=torch.int8, device=gpu)
+            _lib.call("qnn_bn_code_lut", ctypes.byref(bn), c, 1, ctypes.byref(code), _lib.ptr(lut), st)
+            _lib.call("qnn_dwconv_fused_lut", _lib.ptr(xg), n, h, w, pad, hp, wp, cp, c, _lib.ptr(wt), k, k, s, s,
+                      ho, wo, xmin, xs, None if bias is None else _lib.ptr(bias), ctypes.byref(bn), _lib.ptr(lut),
+                      ctypes.byref(code), st)
+            torch.cuda.synchronize()
+        else:
+            _run(xg, geom, wt, bias, bn, 1, None, code, False, st)
+        outs.append(oc.cpu())
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    assert (outs[1][:, 0] == 77).all() and (outs[1][:, :, 0] == 77).all()  # the consumer's padding untouched
+
+
+def test_dwconv_lut_refuses_unsupported(gpu):
+    """Shapes the table kernel is not built for are argument errors, never a silent substitute."""
+    c, n, h = 192, 1, 8  # above 128 channels and not a multiple of 128
+    x = torch.zeros((n, h + 2, h + 2, c), dtype=torch.int8, device=gpu)
+    wt = torch.zeros((9, c), device=gpu)
+    vecs = [torch.ones(c, device=gpu) for _ in range(4)]
+    bn = _lib.BnParams(*[_lib.ptr(v) for v in vecs], 0.9, -0.9, 2.2 / 255, 255.0)
+    oc = torch.zeros((n, h, h, c), dtype=torch.int8, device=gpu)
+    code = _lib.CodeOut(_lib.ptr(oc), c, 0, h, h, 0.2, 1.7 / 255, 255.0)
+    lut = torch.zeros((c, 256), dtype=torch.int8, device=gpu)
+    with pytest.raises(_lib.QnnError, match="qnn_dwconv_fused_lut"):
+        _lib.call("qnn_dwconv_fused_lut", _lib.ptr(x), n, h, h, 1, h + 2, h + 2, c, c, _lib.ptr(wt), 3, 3, 1, 1, h, h,
+                  -0.75, 0.01, None, ctypes.byref(bn), _lib.ptr(lut), ctypes.byref(code), _lib.stream_of(x))
