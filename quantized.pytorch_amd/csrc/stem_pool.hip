@@ -34,7 +34,16 @@ namespace sp {
 
 constexpr int C = 64;    // stem channels (one 64-channel block, 4 MFMA row tiles)
 constexpr int TM = 4;
-constexpr int W = 8;     // waves: each takes every W-th 16-pixel stem tile, all 64 channels
+#ifndef QNN_SP_W
+#define QNN_SP_W 8
+#endif
+#ifndef QNN_SP_DB
+#define QNN_SP_DB 1
+#endif
+constexpr int W = QNN_SP_W;  // waves: each takes every W-th 16-pixel stem tile, all 64 channels
+// 1: two band buffers, the next item's band lands under this item's tiles; 0: one, refilled
+// under this item's pooling (less LDS: more blocks per CU)
+constexpr bool DB = QNN_SP_DB;
 constexpr int NT = 64 * W;
 #ifndef QNN_SP_PR
 #define QNN_SP_PR 4
@@ -171,14 +180,14 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   const float inv_wo = 1.0f / (float)d.wo, inv_pwo = 1.0f / (float)pl.wo;
   const int ct = (C + 31) >> 5;
 
-  for (int buf = 0; it < pl.nitems; it += gridDim.x, buf ^= 1) {
+  for (int buf = 0; it < pl.nitems; it += gridDim.x, buf ^= (DB ? 1 : 0)) {
     const Item q = item(it);
     // this item's band landed (every wave's pieces) and the previous item's pooling is done
     // with the codes: then the next item's band DMA goes into the other buffer, whose last
     // reader (the previous item's tiles) finished before the previous barrier
     wait_vmcnt<0>();
     __syncthreads();
-    if (it + (int)gridDim.x < pl.nitems) issue_band(item(it + gridDim.x), buf ^ 1);
+    if (DB && it + (int)gridDim.x < pl.nitems) issue_band(item(it + gridDim.x), buf ^ 1);
     const int band = pl.lds_band + buf * pl.lds_band_bytes;
     auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
       int qq = t * 16 + (lane & 15);
@@ -242,6 +251,8 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
       }
     }
     __syncthreads();
+    // one band buffer: the tiles are done with it, the next item's band lands under the pooling
+    if (!DB && it + (int)gridDim.x < pl.nitems) issue_band(item(it + gridDim.x), 0);
 
     // ---- 2. pooled (pixel, 16 channels) items, channel groups fastest.  MaxPool2d pads with
     //         -inf: an out-of-image tap is clamped to the nearest in-image row / column, which
@@ -333,7 +344,7 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool&
   off += 16;
   pl.lds_band = off;  // two bands: (2 PR + 1) stem rows read (2 PR) * sh + kh padded input rows, 1 KiB pieces
   pl.lds_band_bytes = (int)cdiv((int64_t)(2 * PR * p.d.sh + p.d.kh) * p.d.wp * p.d.cp, 1024) * 1024;
-  off += 2 * pl.lds_band_bytes;
+  off += (DB ? 2 : 1) * pl.lds_band_bytes;
   pl.lds_codes = off;
   off += (2 * PR + 1) * p.d.wo * C;
   if (off > LDS_MAX) return arg_error("stem max-pool tile needs more than 160 KiB of LDS");
