@@ -182,10 +182,10 @@ CONV_CASES = [
     (96, 80, 3, 2, 1, 1, True, 3, 15, 13),        # ragged, odd sizes, bias
     (128, 128, 3, 2, 1, 128, True, 4, 28, 28),    # depthwise s2
     (32, 32, 3, 1, 1, 32, True, 2, 112, 112),     # depthwise s1 (mobilenet first block)
-    (1024, 1024, 3, 1, 1, 1024, False, 3, 7, 7),  # depthwise, 64 channel groups, 7x7 (tiles cross rows)
-    (16, 16, 3, 2, 1, 16, True, 5, 15, 13),       # depthwise, one channel group, ragged stride 2
+    (1024, 1024, 3, 1, 1, 1024, False, 3, 7, 7),  # depthwise, 1024 channels, 7x7
+    (16, 16, 3, 2, 1, 16, True, 5, 15, 13),       # depthwise, ragged stride 2
     (48, 48, 3, 1, 1, 48, False, 2, 9, 9),        # depthwise, channels not a power of two
-    (24, 24, 3, 1, 1, 24, True, 2, 10, 10),       # depthwise off the MFMA kernel (c % 16 != 0)
+    (24, 24, 3, 1, 1, 24, True, 2, 10, 10),       # depthwise, c % 8 == 0 but not % 16
 ]
 
 
