@@ -402,22 +402,6 @@ int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, 
                          float x_scale, const float* bias, const qnn_bn_params* bn, const int8_t* lut,
                          const qnn_code_out* code0, qnn_stream_t stream);
 
-/* Depthwise QConv2d (groups == c == cout, mobilenet_quantized.py:38-40) as an MFMA contraction
- * over an LDS-staged band of input rows, with the exact decomposition of qnn_qconv2d_fwd
- * (round 4; the engine's and the drop-in module's
- * depthwise when c % 16 == 0 and kh * kw <= 16): desc as for qnn_qconv2d_fwd with cout = c the
- * channels, cp the input code buffer's, wq the depthwise rows of qnn_pack_weight_i8 (cin_g 1,
- * cin_pad 16: tap t's code at byte 16 t), kpad >= 16 * kh * kw; epi's sxsw / sxbw / table /
- * classes / bias as for a conv (qnn_conv_border_table over the depthwise tap sums).
- *   mode 0: out_f32 NCHW fp32 (the drop-in output);
- *   mode 1: RangeBN (bn_neg_min / bn_scale / bn_qmax: its input quantizer) -> the code table
- *           lut[c][256] (qnn_bn_code_lut: RangeBN -> ReLU -> the consumer's quantizer) -> out_code0
- *           (no other output, no residual).
- * Bitwise equal between the two modes through the table, and within the per-layer bar of the
- * reference's fp32 F.conv2d. */
-int qnn_dwconv_mfma_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
-                        qnn_stream_t stream);
-
 /* nn.AvgPool2d(k) over the whole k x k map (resnet_quantized.py:153, mobilenet_quantized.py:157)
  * on fp32 x [n*hw][c] (NHWC, or the C-tile layout when x_tiled): mean = (sum in row-major
  * tap order) / hw; writes out_f32 [n][c]

@@ -94,7 +94,6 @@ SIGNATURES = {
                          c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_int, c_ptr, _PC, c_ptr],
     "qnn_dwconv_fused_lut": [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_float, c_float, c_ptr, _PB, c_ptr, _PC, c_ptr],
-    "qnn_dwconv_mfma_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],
     "qnn_comm_unique_id": [c_ptr, ctypes.c_size_t],

@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .quantize import QConv2d, QLinear, RangeBN, _qmax, border_classes, channel_pad, dw_mfma_ok, float_scale, use_s2d
+from .quantize import QConv2d, QLinear, RangeBN, _qmax, border_classes, channel_pad, float_scale, use_s2d
 
 __all__ = ["Engine"]
 
@@ -222,7 +222,7 @@ class Engine:
         self.launch_meta.append({"kernel": name, "ops": int(ops), "bytes": int(nbytes), "shape": shape})
 
     def _conv(self, conv, src, H, W, bn=None, chain=None, relu=False, outs=(), out_f32=None, out_bncode=None,
-              bncode_tiled=False, mode=1, logits=None, pool=None, depthwise=False):
+              bncode_tiled=False, mode=1, logits=None, pool=None):
         """One fused contraction.  src: (buf, CodeOut, geom) of conv's input codes, or a
         ('s2d', buf, geom) tuple for a space-to-depth stem.  chain: the residual added
         after RangeBN (an _Act.res); out_bncode: RangeBN's input codes (byte C-tile when
@@ -233,7 +233,7 @@ class Engine:
         cin = conv.in_channels if isinstance(conv, QConv2d) else conv.in_features
         cout = conv.out_channels if isinstance(conv, QConv2d) else conv.out_features
         s2d = isinstance(src[0], str) and src[0] == "s2d"
-        pk = conv._pack(depthwise=True) if depthwise else conv._pack(s2d=s2d)
+        pk = conv._pack(s2d=s2d)
         Ho, Wo = (H + 2 * ph - kh) // sh + 1, (W + 2 * pw - kw) // sw + 1
         geom = src[2]
         mn, mx = geom["range"]
@@ -304,11 +304,6 @@ class Engine:
             self._add("qnn_qconv2d_maxpool_fwd", lambda st: _lib.call(
                 "qnn_qconv2d_maxpool_fwd", xp, wp_, dp, ep, pho, pwo, pc, l0, r0, l1, r1, st), ops, nbytes,
                 [M, cout, kh * kw * cin])
-            return Ho, Wo
-        if depthwise:  # one kernel (no tile configurations): qnn_dwconv_mfma_fwd
-            nbytes = geom["nbytes"] + cout * kh * kw + M * cout * len(outs)
-            self._add("qnn_dwconv_fused", lambda st: _lib.call("qnn_dwconv_mfma_fwd", xp, wp_, dp, ep, st), ops, nbytes,
-                      [self.N, Ho, Wo, cout])
             return Ho, Wo
         self.convs.append((len(self.ops), d, e))
         out_b = M * cout * ((4 if out_f32 is not None or mode == 0 else 0) + len(outs) +
@@ -553,34 +548,6 @@ class Engine:
         return untile(src, self.N * H * W, C).reshape(self.N, H, W, C)
 
     # ------------------------------------------------------------------ MobileNet
-    def _dw_fused(self, N, dw, dw_bn, pw, x, a, k, st, p, Ho):
-        """A depthwise layer the MFMA kernel does not take (channels not in 16-groups, > 16 taps):
-        the fp32-FMA kernels (qnn_dwconv_fused / _lut), as the module path's fallback."""
-        xb, xco, xg = self._codes_for(x, dw)
-        pk = dw._pack(depthwise=True)
-        wt = pk.w_hat.t().contiguous()  # [taps][c] for channel-coalesced loads
-        dmn, dmx = xg["range"]
-        x_scale = float_scale(dmn, dmx, dw.num_bits)
-        b = self._bn(dw_bn)
-        pco = self._codes_for(a, pw)[1]
-        self.keep += [pk, wt, xb, pco]
-        dargs = (N, x.H, x.W, p, xg["hp"], xg["wp"], xg["cp"], x.C)
-        dargs2 = (k, k, st, st, Ho, Ho, float(dmn), x_scale)
-        qb, xbp, wtp, br, pr = _lib.ptr(pk.qbias), _lib.ptr(xb), _lib.ptr(wt), ctypes.byref(b), ctypes.byref(pco)
-        ops, nbytes = 2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4
-        # RangeBN -> ReLU -> the pointwise quantizer as the exact per-channel code table where the
-        # 3x3 table kernel takes the layer, else evaluated
-        if k == 3 and st in (1, 2) and x.C % 8 == 0 and (x.C <= 128 or x.C % 128 == 0):
-            lut = torch.empty((x.C, 256), dtype=torch.int8, device=self.dev)
-            _lib.call("qnn_bn_code_lut", br, x.C, 1, pr, _lib.ptr(lut), _lib.stream_of(lut))
-            self.keep.append(lut)
-            lp = _lib.ptr(lut)
-            self._add("qnn_dwconv_fused", lambda s_: _lib.call("qnn_dwconv_fused_lut", xbp, *dargs, wtp, *dargs2, qb,
-                                                                br, lp, pr, s_), ops, nbytes, [N, Ho, Ho, x.C])
-        else:
-            self._add("qnn_dwconv_fused", lambda s_: _lib.call("qnn_dwconv_fused", xbp, *dargs, wtp, *dargs2, qb, br,
-                                                                1, None, pr, s_), ops, nbytes, [N, Ho, Ho, x.C])
-
     def _plan_mobilenet(self, model, hw):
         N = self.N
         self.input = torch.zeros((N, 3, hw, hw), dtype=torch.float32, device=self.dev)
@@ -612,13 +579,34 @@ class Engine:
             k, st, p = dw.kernel_size[0], dw.stride[0], dw.padding[0]
             Ho = (x.H + 2 * p - k) // st + 1
             a = _Act(Ho, Ho, dw.out_channels)
-            if dw_mfma_ok(x.C, k, k, p, p):
-                # the MFMA depthwise kernel (exact decomposition; the module path runs it too), its
-                # RangeBN -> ReLU -> pointwise quantizer as the per-channel code table
-                self._conv(dw, self._codes_for(x, dw), x.H, x.W, bn=dw_bn, relu=True,
-                           outs=[self._codes_for(a, pw)[1]], depthwise=True)
+            xb, xco, xg = self._codes_for(x, dw)
+            pk = dw._pack(depthwise=True)
+            wt = pk.w_hat.t().contiguous()  # [taps][c] for channel-coalesced loads
+            dmn, dmx = xg["range"]
+            x_scale = float_scale(dmn, dmx, dw.num_bits)
+            b = self._bn(dw_bn)
+            pco = self._codes_for(a, pw)[1]
+            self.keep += [pk, wt, xb, pco]
+            dargs = (N, x.H, x.W, p, xg["hp"], xg["wp"], xg["cp"], x.C)
+            dargs2 = (k, k, st, st, Ho, Ho, float(dmn), x_scale)
+            qb, xbp, wtp, br, pr = _lib.ptr(pk.qbias), _lib.ptr(xb), _lib.ptr(wt), ctypes.byref(b), ctypes.byref(pco)
+            # RangeBN -> ReLU -> the pointwise quantizer as the exact per-channel code table (the
+            # conv epilogues' EK_LUT) where the 3x3 table kernel takes the layer, else evaluated
+            lut_ok = k == 3 and st in (1, 2) and x.C % 8 == 0 and (x.C <= 128 or x.C % 128 == 0)
+            if lut_ok:
+                lut = torch.empty((x.C, 256), dtype=torch.int8, device=self.dev)
+                _lib.call("qnn_bn_code_lut", br, x.C, 1, pr, _lib.ptr(lut), _lib.stream_of(lut))
+                self.keep.append(lut)
+                lp = _lib.ptr(lut)
+                self._add("qnn_dwconv_fused", lambda st, xbp=xbp, wtp=wtp, dargs=dargs, dargs2=dargs2, qb=qb, br=br,
+                          pr=pr, lp=lp: _lib.call("qnn_dwconv_fused_lut", xbp, *dargs, wtp, *dargs2, qb, br, lp, pr, st),
+                          2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4,
+                          [N, Ho, Ho, x.C])
             else:
-                self._dw_fused(N, dw, dw_bn, pw, x, a, k, st, p, Ho)
+                self._add("qnn_dwconv_fused", lambda st, xbp=xbp, wtp=wtp, dargs=dargs, dargs2=dargs2, qb=qb, br=br,
+                          pr=pr: _lib.call("qnn_dwconv_fused", xbp, *dargs, wtp, *dargs2, qb, br, 1, None, pr, st),
+                          2 * N * Ho * Ho * x.C * k * k, xg["nbytes"] + N * Ho * Ho * pco.cp + k * k * x.C * 4,
+                          [N, Ho, Ho, x.C])
             # pointwise + bn + relu -> next dw codes (or fp32 for the head)
             out = _Act(Ho, Ho, pw.out_channels)
             if last:

@@ -423,12 +423,6 @@ def border_classes(size, k, stride, pad, out):
     return cls, ranges
 
 
-def dw_mfma_ok(c, kh, kw, ph, pw):
-    """Whether a depthwise layer runs on the MFMA kernel (qnn_dwconv_mfma_fwd: 16-channel groups,
-    at most 16 taps, symmetric padding); the module path and the engine decide alike."""
-    return c % 16 == 0 and kh * kw <= 16 and ph == pw
-
-
 def channel_pad(c):
     """Cp = 16 * 2^j >= c (the kernel's K-chunk addressing needs a power of two)."""
     cp = 16
@@ -762,35 +756,8 @@ class QConv2d(nn.Conv2d, QuantNode, _QLayerMixin):
         mn, mx = rng
         s = float_scale(mn, mx, self.num_bits)
         y = torch.empty((N, C, Ho, Wo), dtype=torch.float32, device=x.device)
-        st = _lib.stream_of(x)
-        if dw_mfma_ok(C, kh, kw, ph, pw):
-            # the MFMA depthwise kernel with the exact decomposition (qnn_dwconv_mfma_fwd), the
-            # one the engine runs (bitwise the same outputs)
-            qmax = _qmax(self.num_bits)
-            s32 = float(np.float32(s))
-            b_x = 128.0 * s32 + float(np.float32(mn))
-            d = _lib.ConvDesc()
-            d.n, d.cout, d.cout_pad, d.ho, d.wo, d.kpad = N, C, pk.cout_pad, Ho, Wo, pk.kpad
-            d.kh, d.kw, d.sh, d.sw, d.cp = kh, kw, sh, sw, channel_pad(C)
-            d.hp, d.wp = H + 2 * ph, W + 2 * pw
-            nbytes = N * d.hp * d.wp * d.cp
-            xq = torch.empty(nbytes + 128, dtype=torch.int8, device=x.device)
-            _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x), _lib.ptr(xq), N, C, H, W, ph, d.cp, -float(mn), s,
-                      qmax, st)
-            d.zero_off = nbytes
-            g = self._geometry(pk, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, x.device)
-            sxsw, sxbw, table = self._epilogue(pk, g, (H, W), s32, b_x, kh, kw)
-            e = _lib.Epilogue()
-            e.mode = 0
-            e.sxsw, e.sxbw, e.table, e.hcls, e.wcls = (sxsw.data_ptr(), sxbw.data_ptr(), table.data_ptr(),
-                                                       g[0].data_ptr(), g[3].data_ptr())
-            e.nwc, e.nclass = g[5], g[2] * g[5]
-            e.bias = None if pk.qbias is None else pk.qbias.data_ptr()
-            e.out_f32 = y.data_ptr()
-            _lib.call("qnn_dwconv_mfma_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
-            return y
         _lib.call("qnn_dwconv2d_fwd", _lib.ptr(x), N, C, H, W, _lib.ptr(pk.w_hat), kh, kw, sh, sw, ph, pw, Ho, Wo,
-                  -float(mn), float(mn), s, _qmax(self.num_bits), _lib.ptr(pk.qbias), _lib.ptr(y), st)
+                  -float(mn), float(mn), s, _qmax(self.num_bits), _lib.ptr(pk.qbias), _lib.ptr(y), _lib.stream_of(x))
         return y
 
 

@@ -185,9 +185,9 @@ CONV_CASES = [
     (1024, 1024, 3, 1, 1, 1024, False, 3, 7, 7),  # depthwise, 1024 channels, 7x7
     (16, 16, 3, 2, 1, 16, True, 5, 15, 13),       # depthwise, ragged stride 2
     (48, 48, 3, 1, 1, 48, False, 2, 9, 9),        # depthwise, channels not a power of two
-    (24, 24, 3, 1, 1, 24, True, 2, 10, 10),       # depthwise off the MFMA kernel (c % 16 != 0)
-    (32, 32, 3, 1, 1, 32, False, 3, 30, 30),      # depthwise, a partial last band (30 rows, bands of 17)
-    (64, 64, 3, 2, 1, 64, True, 2, 57, 57),       # depthwise, odd extent stride 2 (last band clamped)
+    (24, 24, 3, 1, 1, 24, True, 2, 10, 10),       # depthwise, c % 8 == 0 but not % 16
+    (32, 32, 3, 1, 1, 32, False, 3, 30, 30),      # depthwise, 30x30
+    (64, 64, 3, 2, 1, 64, True, 2, 57, 57),       # depthwise, odd extent stride 2
 ]
 
 
