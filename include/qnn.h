@@ -34,7 +34,7 @@ enum {
   QNN_ERR_UNSUPPORTED = 3  /* valid in the reference but not implemented here */
 };
 
-#define QNN_ABI_VERSION 10
+#define QNN_ABI_VERSION 9
 
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
@@ -139,11 +139,6 @@ typedef struct qnn_conv_desc {
   int tile;            /* tile configuration: 0 = chosen by the library's cost model, k + 1 =
                           configuration k of qnn_conv_plan (callers that autotune pass their
                           measured best; the result is identical for every configuration) */
-  int32_t* ksplit_ws;  /* nullable: int32 workspace of the split-K configurations (ABI 10;
-                          qnn_conv_ksplit_bytes); without it they are not built for the call */
-  int* ksplit_cnt;     /* their per-tile arrival counters: zero on entry, left zero */
-  int64_t ksplit_ws_bytes;
-  int ksplit_cnt_n;
 } qnn_conv_desc;
 
 /* Epilogue of the contraction.  Always:
@@ -231,11 +226,6 @@ typedef struct qnn_epilogue {
  * epilogue as described by `epi`.  groups == 1 (depthwise: qnn_dwconv2d_fwd). */
 int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
                     qnn_stream_t stream);
-
-/* Workspace bytes and counters the split-K configurations need for this layer (the largest over
- * them): callers that autotune allocate them once (zeroed counters) and pass them in
- * qnn_conv_desc.ksplit_*; one workspace may serve every launch of a stream. */
-int qnn_conv_ksplit_bytes(const qnn_conv_desc* desc, int64_t* ws_bytes, int* counters);
 
 /* Tile plan qnn_qconv2d_fwd would use for this layer (introspection for benchmarks and
  * profiles; no GPU work): configuration id, block tile (cout x pixels), and the number of

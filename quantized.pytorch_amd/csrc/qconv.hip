@@ -444,12 +444,7 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
 #endif
 }
 
-// KSPLIT (configurations 44-45): the K stages of a tile are split over p.ksplit blocks; each
-// writes its int32 partial accumulators and channel sums to the caller's workspace
-// (qnn_conv_desc.ksplit_ws), and the last of a tile's blocks to arrive (a counter per tile,
-// ksplit_cnt, left at zero) adds the others' -- exact integer sums, any order -- and runs the
-// epilogue: the deep, narrow layers (ResNet layer 3-4 3x3) get several blocks per CU in flight.
-template <class C, int EK, int TAPM, bool MASKED, bool KSPLIT = false>
+template <class C, int EK, int TAPM, bool MASKED>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                       const Params p) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NS = C::NS, W = C::W, TM = C::TM, TN = C::TN;
@@ -470,16 +465,8 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   const int nby = (d.cout + BM - 1) / BM;
   const int nbx = (p.M + BN - 1) / BN;
   const int nblk = nbx * nby;
-  const int S = KSPLIT ? p.ksplit : 1;
-  int t, ks = 0;
-  if constexpr (KSPLIT) {
-    // every K slice of a tile on ONE XCD (blocks are dealt round-robin: block b runs on XCD
-    // b % 8; nblk % 8 == 0 on the host): XCD x owns tiles [x nblk/8, (x+1) nblk/8), so the
-    // slices' partials meet in that XCD's L2 -- no device-scope fence (an L2 write-back) needed
-    const int b = blockIdx.x, xcd = b & 7, li = b >> 3;
-    t = xcd * (nblk >> 3) + li / S;
-    ks = li % S;
-  } else {
+  int t;
+  {
     const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
     t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
   }
@@ -620,11 +607,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     }
   };
 
-  const int nstage_all = d.kpad / BK;
-  // this block's stages [st_lo, nstage): slices of a whole number of ring turns
-  const int slice = KSPLIT ? ((nstage_all + S * NS - 1) / (S * NS)) * NS : nstage_all;
-  const int st_lo = ks * slice;
-  const int nstage = st_lo + slice < nstage_all ? st_lo + slice : nstage_all;
+  const int nstage = d.kpad / BK;
   const bool late = p.stagger && wave >= 4;
 #if QNN_STAMP
   unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, c_iss = 0, c_wait = 0, c_comp = 0;
@@ -636,7 +619,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   // prologue: NS-1 stages in flight
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (st_lo + s < nstage) issue(st_lo + s, s);
+    if (s < nstage) issue(s, s);
 
   // stage st lives in slot st % NS.  Before the barrier of step st every wave waits for
   // its own DMA of stage st (the younger stages st+1 .. st+NS-2 may stay in flight);
@@ -670,7 +653,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   QNN_TS(ts0);
   const unsigned long long c_pro = ts0 - t_begin;
 #endif
-  for (int st = st_lo; st < nstage; st += NS) {  // st_lo % NS == 0: slot = st % NS
+  for (int st = 0; st < nstage; st += NS) {
     step(std::integral_constant<int, 0>{}, st);
     if (st + 1 < nstage) step(std::integral_constant<int, 1>{}, st + 1);
     if (st + 2 < nstage) step(std::integral_constant<int, 2>{}, st + 2);
@@ -681,42 +664,6 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
 #pragma unroll
   for (int j = 0; j < TN; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
   __syncthreads();  // main-loop LDS is reused by the epilogue
-  if constexpr (KSPLIT) {
-    constexpr int PL = TM * TN * 16 + TN;  // int32 per lane: accumulators, channel sums
-    int32_t* ws = p.d.ksplit_ws + (int64_t)t * S * PL * C::NT + tid;
-    int32_t* mine = ws + (int64_t)ks * PL * C::NT;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mine[(int64_t)((i * TN + j) * 16 + r) * C::NT] = acc[i][j][r];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) mine[(int64_t)(TM * TN * 16 + j) * C::NT] = sumq[j];
-    // the stores are acknowledged by this XCD's L2 (the vector L1 writes through) before the
-    // arrival; the arrival counter is an L2 atomic of the same XCD
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* s_flag = reinterpret_cast<int*>(smem);  // the ring's first bytes (free after the loop)
-    if (tid == 0) s_flag[0] = __hip_atomic_fetch_add(p.d.ksplit_cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_flag[0] != S - 1) return;  // another slice of this tile finishes it
-    if (tid == 0) p.d.ksplit_cnt[t] = 0;  // zero again for the next launch (stream-ordered)
-    for (int k2 = 0; k2 < S; ++k2) {
-      if (k2 == ks) continue;
-      const int32_t* other = ws + (int64_t)k2 * PL * C::NT;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            acc[i][j][r] += __builtin_nontemporal_load(other + (int64_t)((i * TN + j) * 16 + r) * C::NT);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) sumq[j] += __builtin_nontemporal_load(other + (int64_t)(TM * TN * 16 + j) * C::NT);
-    }
-    __syncthreads();  // s_flag read by every wave before the epilogue reuses the LDS
-  }
   if (QNN_ABLATE == 3) {
     int z = sumq[0];
 #pragma unroll
@@ -1337,11 +1284,11 @@ static int plan_epi_lds(int lds_main, Params& q) {
   return lds > LDS_MAX ? -1 : lds;
 }
 
-template <class C, int PP, int EK, int TAPM, bool MASKED, int KSP = 1>
+template <class C, int PP, int EK, int TAPM, bool MASKED>
 static int launch_kernel(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   auto kern = [] {
     if constexpr (PP > 0) return qconv_pp_kernel<C, PP, EK, TAPM, MASKED>;
-    else return qconv_kernel<C, EK, TAPM, MASKED, (KSP > 1)>;
+    else return qconv_kernel<C, EK, TAPM, MASKED>;
   }();
   static const hipError_t attr =  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1349,8 +1296,7 @@ static int launch_kernel(const int8_t* x, const int8_t* w, const Params& p, hipS
   Params q = p;
   const int lds = plan_epi_lds<C>(main_lds_bytes<C>(TAPM, MASKED), q);
   if (lds < 0) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
-  q.ksplit = KSP;
-  const int nblk = (int)(cdiv(p.M, C::BN) * cdiv(p.d.cout, C::BM)) * KSP;
+  const int nblk = (int)(cdiv(p.M, C::BN) * cdiv(p.d.cout, C::BM));
   hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q);
   return QNN_OK;
 }
@@ -1433,30 +1379,27 @@ static int launch_band_ek(const int8_t* x, const int8_t* w, const Params& p, hip
   }
 }
 
-template <class C, int PP, int EK, int KSP = 1>
+template <class C, int PP, int EK>
 static int launch_tap(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   constexpr int CPR = C::CPR;
   const int cpt = 1 << p.lgcpt;
-  if (p.d.kmask) {
-    if constexpr (KSP > 1) return arg_error("tile configuration not built for this layer / epilogue kind");
-    else return launch_kernel<C, PP, EK, TAP_LDS, true>(x, w, p, s);
-  }
-  if (cpt >= CPR) return launch_kernel<C, PP, EK, TAP_ONE, false, KSP>(x, w, p, s);
-  if (2 * cpt == CPR) return launch_kernel<C, PP, EK, TAP_TWO, false, KSP>(x, w, p, s);
-  return launch_kernel<C, PP, EK, TAP_LDS, false, KSP>(x, w, p, s);
+  if (p.d.kmask) return launch_kernel<C, PP, EK, TAP_LDS, true>(x, w, p, s);
+  if (cpt >= CPR) return launch_kernel<C, PP, EK, TAP_ONE, false>(x, w, p, s);
+  if (2 * cpt == CPR) return launch_kernel<C, PP, EK, TAP_TWO, false>(x, w, p, s);
+  return launch_kernel<C, PP, EK, TAP_LDS, false>(x, w, p, s);
 }
 
 // PP = k-steps per ping-pong phase (qconv_pp_kernel), 0 = the plain ring loop (qconv_kernel)
-template <class C, int PP = 0, int KSP = 1>
+template <class C, int PP = 0>
 static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return launch_tap<C, PP, EK_NCHW, KSP>(x, w, p, s);
-    case EK_LUT: return launch_tap<C, PP, EK_LUT, KSP>(x, w, p, s);
-    case EK_BNCODE: return launch_tap<C, PP, EK_BNCODE, KSP>(x, w, p, s);
+    case EK_NCHW: return launch_tap<C, PP, EK_NCHW>(x, w, p, s);
+    case EK_LUT: return launch_tap<C, PP, EK_LUT>(x, w, p, s);
+    case EK_BNCODE: return launch_tap<C, PP, EK_BNCODE>(x, w, p, s);
     default:
       // 256x256 blocks + the general chain spill registers: never picked, not built
       if constexpr (C::TM * C::TN >= 8) return arg_error("general fused epilogue not built for this tile");
-      else return launch_tap<C, PP, EK_GEN, KSP>(x, w, p, s);
+      else return launch_tap<C, PP, EK_GEN>(x, w, p, s);
   }
 }
 
@@ -1508,31 +1451,13 @@ static const CfgInfo CFG[NCFG] = {
 };
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
-constexpr int NKSPLIT = 2;
-static const int KSPLITS[NKSPLIT] = {2, 4};  // configurations 44-45: cfg 11's tile, K in 2 / 4 slices
-static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + NKSPLIT; }
+static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count(); }
 static int rb_first() { return NCFG + q16_count(); }
 static int rbp_first() { return NCFG + q16_count() + rb_count(); }
 static int dtab_first() { return rbp_first() + rbp_count(); }
-static int ksplit_first() { return dtab_first() + dtab_count(); }
-static bool cfg_ok(int k, const Params& p);
-
-// split-K: the workspace (int32 per lane: 2x1 32x32 accumulator tiles + channel sums) and counters
-constexpr int KSPLIT_PL = 2 * 1 * 16 + 1, KSPLIT_NT = 256;
-static int64_t ksplit_tiles(const Params& p) { return cdiv(p.M, 128) * cdiv(p.d.cout, 64); }
-static bool ksplit_ok(int S, const Params& p) {
-  const qnn_conv_desc& d = p.d;
-  if (d.kmask || !d.ksplit_ws || !d.ksplit_cnt || !cfg_ok(11, p)) return false;
-  const int64_t tiles = ksplit_tiles(p);
-  if (tiles % 8) return false;  // every XCD a whole number of tiles (the slices of one on one XCD)
-  if (d.ksplit_cnt_n < tiles || d.ksplit_ws_bytes < tiles * S * KSPLIT_PL * KSPLIT_NT * 4) return false;
-  const int nstage = d.kpad / 64, slice = ((nstage + S * 3 - 1) / (S * 3)) * 3;
-  return (S - 1) * slice < nstage;  // every slice holds stages
-}
 
 static bool cfg_ok(int k, const Params& p) {
   if (k >= ncfg_all()) return false;
-  if (k >= ksplit_first()) return ksplit_ok(KSPLITS[k - ksplit_first()], p);
   if (k >= dtab_first()) return dtab_ok(k - dtab_first(), p);
   if (k >= rbp_first()) return rbp_ok(k - rbp_first(), p);
   if (k >= rb_first()) return rb_ok(k - rb_first(), p);
@@ -1550,7 +1475,6 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
-  if (k >= ksplit_first()) return 1e30;  // measured by the autotuner only
   if (k >= dtab_first()) return dtab_cost(k - dtab_first(), p);
   if (k >= rbp_first()) return rbp_cost(k - rbp_first(), p);
   if (k >= rb_first()) return rb_cost(k - rb_first(), p);
@@ -1585,7 +1509,6 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
-  if (k >= ksplit_first()) return k == ksplit_first() ? launch_ek<C11, 0, 2>(x, w, p, s) : launch_ek<C11, 0, 4>(x, w, p, s);
   if (k >= dtab_first()) return dtab_launch(k - dtab_first(), x, w, p, s);
   if (k >= rbp_first()) return rbp_launch(k - rbp_first(), x, w, p, s);
   if (k >= rb_first()) return rb_launch(k - rb_first(), x, w, p, s);
@@ -1664,22 +1587,8 @@ static int conv_params(const qnn_conv_desc& d, const qnn_epilogue& e, Params& p)
 
 extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
-extern "C" int qnn_conv_ksplit_bytes(const qnn_conv_desc* desc, int64_t* ws_bytes, int* counters) {
-  QNN_REQUIRE(desc && ws_bytes && counters, "null pointer");
-  const qnn_conv_desc& d = *desc;
-  QNN_REQUIRE(d.n >= 0 && d.ho > 0 && d.wo > 0 && d.cout > 0, "bad shape");
-  Params p{};
-  p.d = d;
-  p.M = (int)((int64_t)d.n * d.ho * d.wo);
-  const int64_t tiles = ksplit_tiles(p);
-  *ws_bytes = tiles * KSPLITS[NKSPLIT - 1] * KSPLIT_PL * KSPLIT_NT * 4;
-  *counters = (int)tiles;
-  return QNN_OK;
-}
-
 extern "C" const char* qnn_conv_tile_kernel(int k) {
   if (k < 0 || k >= ncfg_all()) return nullptr;
-  if (k >= ksplit_first()) return "qconv_kernel";
   if (k >= dtab_first()) return "qconv_dtab_kernel";
   if (k >= rbp_first()) return "qconv_rbp_kernel";
   if (k >= rb_first()) return k - rb_first() < rb_count() - direct_count() ? "qconv_rb_kernel" : "qconv_direct_kernel";
@@ -1699,8 +1608,7 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   int tbm, tbn;
-  if (k >= ksplit_first()) tbm = CFG[11].bm, tbn = CFG[11].bn;
-  else if (k >= dtab_first()) dtab_tile(k - dtab_first(), &tbm, &tbn);
+  if (k >= dtab_first()) dtab_tile(k - dtab_first(), &tbm, &tbn);
   else if (k >= rbp_first()) rbp_tile(k - rbp_first(), &tbm, &tbn);
   else if (k >= rb_first()) rb_tile(k - rb_first(), &tbm, &tbn);
   else if (k >= NCFG) q16_tile(k - NCFG, &tbm, &tbn);
@@ -1708,8 +1616,7 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
   if (nblk)
-    *nblk = k >= ksplit_first() ? (int)(ksplit_tiles(p) * KSPLITS[k - ksplit_first()])
-            : k >= dtab_first() ? (int)dtab_blocks(k - dtab_first(), p)
+    *nblk = k >= dtab_first() ? (int)dtab_blocks(k - dtab_first(), p)
             : k >= rbp_first() ? (int)rbp_blocks(k - rbp_first(), p)
             : k >= rb_first() ? (int)rb_blocks(k - rb_first(), p)
                               : (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm));
@@ -1756,7 +1663,7 @@ extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue*
   if (rc != QNN_OK) return rc;
   const int k = pick_cfg(p);
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
-  QNN_REQUIRE(k >= rb_first() && k < ksplit_first(), "occupancy is reported for the resident-band and direct-fragment configurations");
+  QNN_REQUIRE(k >= rb_first(), "occupancy is reported for the resident-band and direct-fragment configurations");
   Occ o{0, 0, 0};
   const int r = k >= dtab_first()  ? dtab_launch(k - dtab_first(), nullptr, nullptr, p, nullptr, &o)
                 : k >= rbp_first() ? rbp_launch(k - rbp_first(), nullptr, nullptr, p, nullptr, &o)

@@ -40,7 +40,6 @@ struct Params {
   int epi_off;   // LDS byte offset of the epilogue data (stage_epi)
   int epi_early; // 1: staged by LDS-DMA at kernel start (lands during the main loop), 0: after it
   int scr_off;   // LDS byte offset of the NCHW transpose scratch (used after the main loop)
-  int ksplit;    // split-K configurations: K slices per tile
 };
 
 struct CodeDst {

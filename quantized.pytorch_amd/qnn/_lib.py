@@ -16,8 +16,8 @@ import torch  # noqa: F401  (binds the process HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QNN_LIB") or os.path.join(_HERE, "libqnn_hip.so")  # QNN_LIB: diagnostic builds
 
-ABI_VERSION = 10
-CONV_TILES = 46  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
+ABI_VERSION = 9
+CONV_TILES = 44  # tile configurations of qnn_qconv2d_fwd (qnn_conv_desc.tile = k + 1); == qnn_conv_tile_count()
 
 c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -25,9 +25,7 @@ c_int, c_i64, c_float, c_ptr = ctypes.c_int, ctypes.c_int64, ctypes.c_float, cty
 class ConvDesc(ctypes.Structure):
     """qnn_conv_desc (include/qnn.h)."""
     _fields_ = [(n, c_int) for n in ("n", "hp", "wp", "cp", "zero_off", "cout", "cout_pad", "kh", "kw", "sh", "sw",
-                                     "ho", "wo", "kpad")] + [("kmask", c_ptr), ("tile", c_int), ("ksplit_ws", c_ptr),
-                                                             ("ksplit_cnt", c_ptr), ("ksplit_ws_bytes", c_i64),
-                                                             ("ksplit_cnt_n", c_int)]
+                                     "ho", "wo", "kpad")] + [("kmask", c_ptr), ("tile", c_int)]
 
 
 class ResLink(ctypes.Structure):
@@ -82,7 +80,6 @@ SIGNATURES = {
                            c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_conv_border_table": [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_float, c_ptr, c_ptr],
     "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
-    "qnn_conv_ksplit_bytes": [ctypes.POINTER(ConvDesc), ctypes.POINTER(c_i64), ctypes.POINTER(c_int)],
     "qnn_conv_plan": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_conv_occupancy": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -114,7 +114,6 @@ class Engine:
                 self._plan_resnet(model, hw)
             else:
                 raise NotImplementedError("qnn.Engine supports resnet_quantized and mobilenet_quantized models")
-        self._ksplit_workspace()
         self.tiles = None
         fixed = os.environ.get("QNN_ENGINE_TILES")  # "k,k,..." per contraction (reproducible profiles)
         if fixed:
@@ -150,24 +149,6 @@ class Engine:
             self._capture()
 
     # ------------------------------------------------------------------ buffers
-    def _ksplit_workspace(self):
-        """One int32 workspace and zeroed per-tile counters for the split-K configurations,
-        sized for the largest contraction of the plan and shared by all of them (the launches
-        are stream-ordered; each leaves the counters at zero)."""
-        need, ntile = 0, 0
-        for _i, d, _e in self.convs:
-            b, c = ctypes.c_int64(), ctypes.c_int()
-            _lib.call("qnn_conv_ksplit_bytes", ctypes.byref(d), ctypes.byref(b), ctypes.byref(c))
-            need, ntile = max(need, b.value), max(ntile, c.value)
-        if need == 0:
-            return
-        ws = torch.empty(need // 4, dtype=torch.int32, device=self.dev)
-        cnt = torch.zeros(ntile, dtype=torch.int32, device=self.dev)
-        self.keep += [ws, cnt]
-        for _i, d, _e in self.convs:
-            d.ksplit_ws, d.ksplit_cnt = ws.data_ptr(), cnt.data_ptr()
-            d.ksplit_ws_bytes, d.ksplit_cnt_n = need, ntile
-
     def _codes_for(self, act, conv):
         """Padded NHWC8 input buffer of `conv` holding `act`'s codes (allocated once,
         zero border + 128-byte zero page); returns (tensor, CodeOut, geometry)."""
