@@ -167,6 +167,11 @@ double rbp_cost(int k, const Params& p);
 int64_t rbp_blocks(int k, const Params& p);
 int rbp_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
 
+// qconv_direct.hip's classifier-head configuration (the last id)
+bool dhead_ok(const Params& p);
+int64_t dhead_blocks(const Params& p);
+int dhead_launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
+
 // qconv_direct.hip's table-epilogue configurations (ids after the two-team ones)
 int dtab_count();
 void dtab_tile(int k, int* bm, int* bn);

@@ -351,6 +351,35 @@ int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipS
 }
 
 // ---------------------------------------------------------------------------------------------
+// The classifier head (configuration 44, round 4): QLinear / 1x1 on few pixels -- the batch --
+// with K = 512 or 1024 (ResNet-18 / MobileNet fc, resnet_quantized.py:154, mobilenet_quantized.py
+// :158) and the drop-in fp32 output.  The ring configurations tile it 64 channels x 128 pixels:
+// 16 blocks for a 128-image batch, each walking 8-16 K stages -- 16 of 256 CUs busy.  Here a
+// block is 16 channels x 64 pixels (4 waves x one 16-pixel tile), every K fragment one global
+// load straight into VGPRs (the direct kernel, all KS steps resident): 126 blocks at b128, each a
+// few microseconds.  cout need not be a multiple of 16 (the NCHW stores are masked per channel).
+namespace dh {
+using DH = dk::Cfg<1, 1>;
+constexpr int BN = 64, CB = 16;
+}  // namespace dh
+
+bool dhead_ok(const Params& p) {
+  const qnn_conv_desc& d = p.d;
+  if (epi_kind(p.e) != EK_NCHW || p.taps != 1 || d.kmask || d.cp % 16 || p.M >= (1 << 24)) return false;
+  if (d.kpad != 512 && d.kpad != 1024) return false;
+  if (p.taps * d.cp > d.kpad || d.cout_pad < (int)cdiv(d.cout, dh::CB) * dh::CB) return false;
+  return dk::epi_bytes(p, 64) + 16 + 4 * (d.ho + d.wo) <= LDS_MAX;
+}
+
+int64_t dhead_blocks(const Params& p) { return cdiv(p.M, dh::BN) * cdiv(p.d.cout, dh::CB); }
+
+int dhead_launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  if (!dhead_ok(p)) return arg_error("tile configuration not built for this layer / epilogue kind");
+  return p.d.kpad == 512 ? dk::launch<dh::DH, EK_NCHW, false, 8>(x, w, p, s, occ)
+                         : dk::launch<dh::DH, EK_NCHW, false, 16>(x, w, p, s, occ);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Table-epilogue configurations (ids after the two-team ones, qnn_conv_tile_kernel
 // "qconv_dtab_kernel"): the general chain -- RangeBN, the residual (fp32 and/or a code chain of
 // up to four links), ReLU, codes / fp32 out -- of the short-K 1x1 layers, ResNet-50's expand

@@ -99,10 +99,13 @@ def test_tile_kernel_families(lib):
     # families are contiguous id ranges; round 4 appended the two-team resident band, then the
     # table-epilogue direct configurations (ids of earlier families never move)
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
-    assert len(runs) == len(set(runs)) + 1  # the ring family is split by the ping-pong ids 6-9
-    assert len(_lib.tile_ids("qconv_direct_kernel")) == 5
+    # the ring family is split by the ping-pong ids 6-9, the direct family by ids 40-43 (the
+    # classifier head, 44, is a direct-fragment configuration appended in round 4)
+    assert len(runs) == len(set(runs)) + 2
+    assert len(_lib.tile_ids("qconv_direct_kernel")) == 6 and _lib.tile_ids("qconv_direct_kernel")[-1] == 44
     assert _lib.tile_ids("qconv_rbp_kernel") == [40, 41]
-    assert fams[-1] == "qconv_dtab_kernel" and _lib.tile_ids("qconv_dtab_kernel") == [42, 43]
+    assert _lib.tile_ids("qconv_dtab_kernel") == [42, 43]
+    assert fams[-1] == "qconv_direct_kernel" and len(fams) == 45
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 

@@ -40,6 +40,8 @@ SHAPES = [
     ("ds_1x1_s2_256_512", 256, 512, 1, 2, 0, 4, 14, 14),
     ("stem_7x7_s2", 3, 64, 7, 2, 3, 2, 224, 224),
     ("fc_2048_1000", 2048, 1000, 0, 1, 0, 37, 1, 1),
+    ("fc_512_1000_b128", 512, 1000, 0, 1, 0, 128, 1, 1),   # ResNet-18 head (configuration 44)
+    ("fc_1024_1000_b37", 1024, 1000, 0, 1, 0, 37, 1, 1),   # MobileNet head, ragged batch
 ]
 
 
