@@ -193,10 +193,13 @@ def in_graph_times(engine, reps):
     the launches of one kind (every contraction, or every depthwise conv, ...) are captured in
     plan order as a hipGraph of their own, which is replayed `reps` times between two events
     recorded on torch's current stream (the stream the replay runs on).  Each launch thus runs
-    once per replay in the same order, on the same buffers and with the same cache history
-    per forward as inside the full graph -- no back-to-back repeats of one launch over warm
-    operands -- and the figure includes the in-graph launch boundaries (~1 us each), so it
-    bounds the kernels' own rate from below.  Returns ({kind: ms per forward}, conv ms)."""
+    once per replay, in plan order and on the engine's own buffers -- no back-to-back repeats
+    of one launch over warm operands -- but WITHOUT the other launch kinds in between (input
+    quantizer, pooling, depthwise ...), so the L2 / Infinity-Cache contents a launch meets are
+    not exactly those of the full graph; tools/trace_check.py cross-checks the figure against
+    the full-graph trace of the same command.  It includes the in-graph launch boundaries
+    (~1 us each), so it bounds the kernels' own rate from below.  Returns ({kind: ms per
+    forward}, conv ms)."""
     out = {}
     for name in dict.fromkeys(engine.launch_names):
         g, _n = engine.capture_subset([name])

@@ -16,16 +16,16 @@
 //   arbitration, so it finishes its K loop first and runs its epilogue (VALU, LDS, stores)
 //   while team 1's MFMAs still fill the pipe.  Only team 1's epilogue is exposed.
 // * the band lands in K-group chunks (planes 2g, 2g+1 = input channels [64g, 64g + 64) of every
-//   band pixel).  Team 1 is its loader: it issues every chunk's LDS-DMA at kernel start, then
-//   waits for them in order (counted vmcnt) and publishes each through an LDS counter; every
-//   wave polls the counter before its first step of a chunk.  Team 0 loads only weights, so
-//   none of its (in-order) vmcnt waits ever waits for the band, and it starts computing as
-//   soon as chunk 0 is published -- alone on the matrix pipes until team 1 has finished the
-//   prologue.  That head start is the stagger.  No workgroup barrier after the start.
-// * sum_valid(q'_x): as each chunk lands, team 1 sums the bytes each lane moved (v_dot4
-//   against 1s) into a per-band-pixel channel sum in LDS, then one lane per output pixel sums
-//   its taps; team 1 also stages the epilogue data (per-channel vectors, border table, code
-//   LUT) -- all before its own K loop.
+//   band pixel).  EVERY wave of both teams loads it: each wave issues ppp / 4 of a chunk's
+//   2 ppp 1 KiB pieces (issue_own; chunk 0 in the prologue, chunk g + 1 during taps 0-3 of
+//   chunk g), waits for its own pieces with a counted vmcnt that leaves its younger weight
+//   loads in flight (so a wave's in-order vmcnt waits do cover its own band DMA), and adds 1
+//   to the chunk's LDS counter; every wave polls for all 8 arrivals before its first step of a
+//   chunk.  No workgroup barrier after the start.  The stagger is team 0's priority only.
+// * sum_valid(q'_x): as its pieces of a chunk land, every wave sums the bytes each of its lanes
+//   moved (v_dot4 against 1s) into a per-band-pixel channel sum in LDS (sum_chunk); after the
+//   K loop one team-0 lane per output pixel sums its taps.  Each team stages its own epilogue
+//   data (per-channel vectors, border table, code LUT) by LDS-DMA during its last chunk.
 #include <stdlib.h>
 
 #include <type_traits>

@@ -109,12 +109,23 @@ def build_engine(model, batch, group=None, **kw):
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return Engine(model, batch, **kw)
     rank = dist.get_rank(group)
-    eng = Engine(model, batch, **kw) if rank == 0 else None
-    n = torch.tensor([len(eng.tiles) if eng is not None else 0], dtype=torch.int64)
+    eng, err = None, None
+    if rank == 0:
+        try:
+            eng = Engine(model, batch, **kw)
+        except Exception as ex:  # noqa: BLE001 -- re-raised below, after the other ranks learn of it
+            err = ex
+    # n = -1 tells the other ranks that rank 0 failed, so no rank is left waiting in the
+    # second broadcast; every rank then raises
+    n = torch.tensor([len(eng.tiles) if eng is not None else -1 if err is not None else 0], dtype=torch.int64)
     dev_comm = dist.get_backend(group) == "nccl"
     if dev_comm:
         n = n.cuda()
     dist.broadcast(n, 0, group=group)
+    if int(n.item()) < 0:
+        if err is not None:
+            raise err
+        raise RuntimeError("build_engine: rank 0 failed to build its Engine (see rank 0's error)")
     t = torch.tensor([k for k, _ in eng.tiles] if eng is not None else [0] * int(n.item()), dtype=torch.int64)
     if dev_comm:
         t = t.cuda()

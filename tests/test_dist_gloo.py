@@ -276,3 +276,38 @@ def test_allreduce_calibration_weights_collective(weights, expect):
         assert p.exitcode == 0
     res = sorted(q.get(timeout=10) for _ in range(2))
     assert [r[1:] for r in res] == [expect, expect]
+
+
+def _build_engine_fail_worker(rank, world, port, q):
+    import qnn.engine as E
+    from qnn.dist import build_engine
+
+    class _Boom:  # stands in for qnn.Engine: rank 0's autotune fails (e.g. no tile configuration)
+        def __init__(self, *a, **k):
+            raise RuntimeError("no tile configuration")
+
+    E.Engine = _Boom
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        build_engine(torch.nn.Identity(), 4)
+        q.put((rank, "returned"))
+    except RuntimeError as ex:
+        q.put((rank, "raised", "no tile configuration" in str(ex) if rank == 0 else True))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_build_engine_rank0_failure_raises_on_every_rank():
+    """rank 0's Engine construction failing must not leave the other ranks waiting in
+    the tile-table broadcast -- every rank raises after the one collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_build_engine_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert sorted(q.get(timeout=10) for _ in range(2)) == [(0, "raised", True), (1, "raised", True)]

@@ -85,3 +85,29 @@ def test_dtab_refuses_other_epilogue_kinds(gpu):
         d.tile = 0
     torch.cuda.synchronize()
     assert built and refused
+
+
+def test_dtab_general_geometry_bitwise(gpu):
+    """the per-pixel border-class lookup (nclass > 1) and the non-DENSE instantiation
+    of the table epilogue are exercised -- CIFAR ResNet-18's 3x3 general-chain convolutions (16 and
+    32 input channels, zero-padded consumer outputs) with configurations 42 and 43 forced, bitwise
+    against the module path.  (No model here has a stride-2 general-chain contraction: a block's
+    strided conv is its first, whose epilogue is the code table -- refused by these configurations.)"""
+    from qnn.engine import Engine
+    d = load_fixture("model_resnet18_cifar")
+    model, _ = build_model(d)
+    batch = 6
+    x = synthetic.input_batch((batch,) + tuple(d["config"]["shape"][1:]), 93)
+    model = model.to(gpu)
+    xg = x.to(gpu)
+    feat = _module_feat(model, xg).permute(0, 2, 3, 1)
+    for t in _lib.tile_ids("qconv_dtab_kernel"):
+        eng = Engine(model, batch=batch, graph=False, tile=t)
+        forced = [(dd, ee) for (k, _), (_n, dd, ee) in zip(eng.tiles, eng.convs) if dd.tile == t + 1]
+        assert any(dd.kh == 3 and ee.nclass > 1 for dd, ee in forced), \
+            f"configuration {t}: no 3x3 with border classes forced ({[(dd.kh, ee.nclass) for dd, ee in forced]})"
+        assert any(ee.code0_pad > 0 for dd, ee in forced), f"configuration {t}: no padded consumer output"
+        for rep in range(2):
+            eng(xg)
+            torch.cuda.synchronize()
+            assert torch.equal(eng.head_input, feat), f"configuration {t} run {rep}: engine != module path"

@@ -15,7 +15,7 @@ NAMES = ["void qnn::quantize_s2d_x2_kernel<1, 3>(int)", "void qnn::sp::stem_pool
 DUR = [20_000, 100_000, 50_000, 5_000]  # ns
 
 
-def _write(tmp, steps=20, warmup=5, conv_frac=None, ms_per_step=None):
+def _write(tmp, steps=20, warmup=5, conv_frac=None, ms_per_step=None, lead=None):
     rows, t = [], 1_000_000
     def emit(name, dur):
         nonlocal t
@@ -23,6 +23,8 @@ def _write(tmp, steps=20, warmup=5, conv_frac=None, ms_per_step=None):
         t += dur + 1_000
     for _ in range(3):  # autotune: one conv repeated
         emit(NAMES[2], 60_000)
+    if lead is not None:  # a launch before the replays with the name of a block's last one
+        emit(NAMES[lead], DUR[lead])
     for _ in range(1 + warmup + steps):  # capture warm-up + the replays
         for n, dur in zip(NAMES, DUR):
             emit(n, dur)
@@ -66,3 +68,15 @@ def test_trace_check_refuses_stale_trace(tmp_path):
     assert trace_check.main(trace, bj, str(tmp_path / "o.json")) == 1
     trace, bj = _write(str(tmp_path), conv_frac=0.2)  # the bench's frac disagrees with the trace
     assert trace_check.main(trace, bj, str(tmp_path / "o2.json")) == 1
+
+
+def test_trace_check_anchors_on_the_input_quantizer(tmp_path):
+    """A leading launch named like a block's last one makes a rotated run periodic too; the
+    blocks must still start at the forward's first launch."""
+    import trace_check
+    trace, bj = _write(str(tmp_path), lead=3)
+    out = str(tmp_path / "out.json")
+    assert trace_check.main(trace, bj, out) == 0
+    r = json.load(open(out))
+    assert r["launches"][0]["kernel"].startswith("quantize_s2d")
+    assert [x["us"] for x in r["launches"]] == [20.0, 100.0, 50.0, 5.0]

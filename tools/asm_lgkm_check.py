@@ -8,12 +8,23 @@ read's destination VGPRs (a copy `v_mov`, a spill, a reuse of the register) sees
 data.  This tool simulates the in-order LGKM queue per basic block and reports every
 such access.
 
+Scalar-memory loads (s_load_*, s_buffer_load_*, s_memtime / s_memrealtime) count in
+LGKM_CNT too but return OUT OF ORDER.  The tool tracks every one issued since
+the last lgkmcnt(0) and reports each hand-counted (inline-asm) `lgkmcnt(N>0)` issued while
+one may be in flight.  Whether such a wait is a hazard depends on what it is meant to cover:
+for LDS reads counted over LDS reads only it is still exact -- L LDS + K scalar ops
+outstanding, waiting until <= N remain forces >= L + K - N completions, >= L - N of them LDS
+ones, and LDS ops complete in order -- so the oldest L - N reads are done whatever the scalar
+loads do; it would be a hazard only for a wait meant to cover the scalar load itself or
+counted with the scalar load in N.  Both counts are printed.
+
 usage: python tools/asm_lgkm_check.py file.s [--verbose]
 """
 import re
 import sys
 
 VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+SMEM = ("s_load_", "s_buffer_load_", "s_memtime", "s_memrealtime", "s_scratch_load", "s_dcache_")
 KERNEL = re.compile(r"^(_Z\S+):")
 
 
@@ -46,9 +57,12 @@ def split_operands(ins):
 def check(path, verbose=False):
     kern = None
     pending = []  # list of (dest regs, line no) of hand-counted asm reads, oldest first
+    smem = []  # line numbers of scalar-memory loads possibly in flight (since the last lgkmcnt(0))
     in_asm = False
     issues = 0
     nreads = 0
+    smem_waits = 0  # hand-counted lgkmcnt(N > 0) issued while a scalar load may be in flight
+    hand_waits = 0
     with open(path) as f:
         lines = f.readlines()
     for no, raw in enumerate(lines, 1):
@@ -57,6 +71,7 @@ def check(path, verbose=False):
         if m:
             kern = m.group(1)
             pending = []
+            smem = []
             continue
         if raw.strip() == ";;#ASMSTART":
             in_asm = True
@@ -69,6 +84,8 @@ def check(path, verbose=False):
         if line.endswith(":"):  # a label: conservatively keep the queue (fallthrough)
             continue
         op = line.split()[0]
+        if op.startswith(SMEM):
+            smem.append(no)
         if in_asm:
             if op.startswith("ds_read"):
                 d = regs(line.split(",")[0])
@@ -78,6 +95,14 @@ def check(path, verbose=False):
                 mm = re.search(r"lgkmcnt\((\d+)\)", line)
                 if mm:
                     n = int(mm.group(1))
+                    hand_waits += 1
+                    if n > 0 and smem:
+                        smem_waits += 1
+                        if verbose:
+                            print(f"{path}:{no}: {(kern or '')[:90]}: hand-counted lgkmcnt({n}) with scalar loads "
+                                  f"possibly in flight (issued at lines {smem[-4:]})")
+                    if n == 0:
+                        smem = []
                     while len(pending) > n:
                         pending.pop(0)
             continue
@@ -85,6 +110,8 @@ def check(path, verbose=False):
             mm = re.search(r"lgkmcnt\((\d+)\)", line)
             if mm:
                 n = int(mm.group(1))
+                if n == 0:
+                    smem = []
                 while len(pending) > n:
                     pending.pop(0)
             continue
@@ -106,7 +133,8 @@ def check(path, verbose=False):
                 issues += 1
                 kind = "reads" if hit_r else "writes"
                 print(f"{path}:{no}: {kern[:90]}: `{line}` {kind} v{sorted(hit_r or hit_w)} of the LDS read at line {rno} before its lgkmcnt wait")
-    print(f"checked {nreads} hand-counted LDS reads: {issues} premature accesses")
+    print(f"checked {nreads} hand-counted LDS reads: {issues} premature accesses; "
+          f"{smem_waits} of {hand_waits} hand-counted lgkmcnt waits issued with a scalar load possibly in flight")
     return issues
 
 
