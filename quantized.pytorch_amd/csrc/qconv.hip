@@ -1451,14 +1451,16 @@ static const CfgInfo CFG[NCFG] = {
 };
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
-static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1; }
+static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1 + pb_count(); }
 static int rb_first() { return NCFG + q16_count(); }
 static int rbp_first() { return NCFG + q16_count() + rb_count(); }
 static int dtab_first() { return rbp_first() + rbp_count(); }
 static int dhead_id() { return dtab_first() + dtab_count(); }  // configuration 44: the classifier head
+static int pb_first() { return dhead_id() + 1; }                 // configurations 45-49: persistent band
 
 static bool cfg_ok(int k, const Params& p) {
   if (k >= ncfg_all()) return false;
+  if (k >= pb_first()) return pb_ok(k - pb_first(), p);
   if (k == dhead_id()) return dhead_ok(p);
   if (k >= dtab_first()) return dtab_ok(k - dtab_first(), p);
   if (k >= rbp_first()) return rbp_ok(k - rbp_first(), p);
@@ -1477,6 +1479,7 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
+  if (k >= pb_first()) return pb_cost(k - pb_first(), p);
   if (k == dhead_id()) return p.M <= 256 ? 0.0 : 1e30;  // measured: ahead of cfg 11 at b128 (6.4 vs 11.2 us), behind at b512
   if (k >= dtab_first()) return dtab_cost(k - dtab_first(), p);
   if (k >= rbp_first()) return rbp_cost(k - rbp_first(), p);
@@ -1512,6 +1515,7 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (k >= pb_first()) return pb_launch(k - pb_first(), x, w, p, s);
   if (k == dhead_id()) return dhead_launch(x, w, p, s);
   if (k >= dtab_first()) return dtab_launch(k - dtab_first(), x, w, p, s);
   if (k >= rbp_first()) return rbp_launch(k - rbp_first(), x, w, p, s);
@@ -1593,6 +1597,7 @@ extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
 extern "C" const char* qnn_conv_tile_kernel(int k) {
   if (k < 0 || k >= ncfg_all()) return nullptr;
+  if (k >= pb_first()) return "qconv_pb_kernel";
   if (k == dhead_id()) return "qconv_direct_kernel";
   if (k >= dtab_first()) return "qconv_dtab_kernel";
   if (k >= rbp_first()) return "qconv_rbp_kernel";
@@ -1613,7 +1618,8 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   int tbm, tbn;
-  if (k == dhead_id()) tbm = 16, tbn = 64;
+  if (k >= pb_first()) pb_tile(k - pb_first(), &tbm, &tbn);
+  else if (k == dhead_id()) tbm = 16, tbn = 64;
   else if (k >= dtab_first()) dtab_tile(k - dtab_first(), &tbm, &tbn);
   else if (k >= rbp_first()) rbp_tile(k - rbp_first(), &tbm, &tbn);
   else if (k >= rb_first()) rb_tile(k - rb_first(), &tbm, &tbn);
@@ -1622,7 +1628,8 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
   if (nblk)
-    *nblk = k == dhead_id() ? (int)dhead_blocks(p)
+    *nblk = k >= pb_first() ? (int)pb_blocks(k - pb_first(), p)
+            : k == dhead_id() ? (int)dhead_blocks(p)
             : k >= dtab_first() ? (int)dtab_blocks(k - dtab_first(), p)
             : k >= rbp_first() ? (int)rbp_blocks(k - rbp_first(), p)
             : k >= rb_first() ? (int)rb_blocks(k - rb_first(), p)
@@ -1672,7 +1679,8 @@ extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue*
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   QNN_REQUIRE(k >= rb_first(), "occupancy is reported for the resident-band and direct-fragment configurations");
   Occ o{0, 0, 0};
-  const int r = k == dhead_id()    ? dhead_launch(nullptr, nullptr, p, nullptr, &o)
+  const int r = k >= pb_first()    ? pb_launch(k - pb_first(), nullptr, nullptr, p, nullptr, &o)
+                : k == dhead_id()    ? dhead_launch(nullptr, nullptr, p, nullptr, &o)
                 : k >= dtab_first()  ? dtab_launch(k - dtab_first(), nullptr, nullptr, p, nullptr, &o)
                 : k >= rbp_first() ? rbp_launch(k - rbp_first(), nullptr, nullptr, p, nullptr, &o)
                                    : rb_launch(k - rb_first(), nullptr, nullptr, p, nullptr, &o);

@@ -180,6 +180,14 @@ double dtab_cost(int k, const Params& p);
 int64_t dtab_blocks(int k, const Params& p);
 int dtab_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
 
+// qconv_pb.hip's persistent-band configurations (ids after the classifier head)
+int pb_count();
+void pb_tile(int k, int* bm, int* bn);
+bool pb_ok(int k, const Params& p);
+double pb_cost(int k, const Params& p);
+int64_t pb_blocks(int k, const Params& p);
+int pb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
+
 // stem_pool.hip: the space-to-depth stem conv fused with RangeBN's input codes and
 // MaxPool2d(3, 2, 1) (qnn_qconv2d_maxpool_fwd)
 int stem_pool_launch(const int8_t* x, const int8_t* w, const Params& p, int pool_ho, int pool_wo, uint8_t* out_code,

@@ -95,7 +95,8 @@ def test_tile_kernel_families(lib):
     from qnn import _lib
     fams = [_lib.tile_kernel(k) for k in range(_lib.CONV_TILES)]
     assert set(fams) == {"qconv_kernel", "qconv_pp_kernel", "qconv_band_kernel", "qconv16_kernel",
-                         "qconv_rb_kernel", "qconv_direct_kernel", "qconv_rbp_kernel", "qconv_dtab_kernel"}
+                         "qconv_rb_kernel", "qconv_direct_kernel", "qconv_rbp_kernel", "qconv_dtab_kernel",
+                         "qconv_pb_kernel"}
     # families are contiguous id ranges; round 4 appended the two-team resident band, then the
     # table-epilogue direct configurations (ids of earlier families never move)
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
@@ -105,7 +106,9 @@ def test_tile_kernel_families(lib):
     assert len(_lib.tile_ids("qconv_direct_kernel")) == 6 and _lib.tile_ids("qconv_direct_kernel")[-1] == 44
     assert _lib.tile_ids("qconv_rbp_kernel") == [40, 41]
     assert _lib.tile_ids("qconv_dtab_kernel") == [42, 43]
-    assert fams[-1] == "qconv_direct_kernel" and len(fams) == 45
+    assert fams[44] == "qconv_direct_kernel"
+    # round 5 appended the persistent-band configurations 45-49
+    assert _lib.tile_ids("qconv_pb_kernel") == [45, 46, 47, 48, 49] and len(fams) == 50
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 

@@ -3,6 +3,8 @@
 # steps:
 #   tests              the whole -m gpu suite
 #   test:PATH[::K]     one test file / node
+#   pyt:ARGS           pytest -m gpu with ARGS (comma-separated; '+' inside an argument is a space,
+#                      e.g. pyt:tests/test_gpu_tiles.py,-k,45+or+46)
 #   smoke              __graft_entry__.smoke()
 #   bench[:ARGS]       python bench.py ARGS  (ARGS: comma-separated, e.g. bench:--depth,50,--batch,256)
 #   prof:MODEL:DEPTH:BATCH   tools/gpu_prof.sh (kernel trace of 10 graph replays + PMC traffic)
@@ -27,6 +29,9 @@ for S in "$@"; do
     test) N=$(echo "$ARG" | tr '/:' '__')
           timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu $ARG > $O/test_$N.log 2>&1
           rc=$?; tail -3 $O/test_$N.log ;;
+    pyt) IFS=, read -r -a PA <<< "$ARG"; PA=("${PA[@]//+/ }")
+         timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu "${PA[@]}" > $O/pyt.log 2>&1
+         rc=$?; tail -5 $O/pyt.log ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
            rc=$?; tail -1 $O/smoke.log ;;
     bench) N=$(echo "$ARGS" | tr -d ' -' | head -c 40)
