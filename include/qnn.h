@@ -227,6 +227,18 @@ typedef struct qnn_epilogue {
 int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
                     qnn_stream_t stream);
 
+/* The drop-in QConv2d forward from the module's own fp32 NCHW input (quantize.py:314-354: the
+ * input quantizer, then the conv), one launch: the persistent-band kernel quantizes each input
+ * band into LDS (x + neg_min over scale, round, clamp to [0, qmax]: bitwise the codes
+ * qnn_quantize_nchw_to_nhwc8 writes) instead of reading a code tensor.  desc is the layer's
+ * descriptor for that code tensor (hp = h + 2 pad, wp = w + 2 pad, cp >= c); epi mode 0 (fp32
+ * NCHW out).  tile: 0 = the cheapest persistent-band configuration that fits, k + 1 =
+ * configuration k.  Returns QNN_ERR_UNSUPPORTED when none fits (3x3 on 64 or 128 padded input
+ * channels, stride 1 or 2): the caller quantizes and calls qnn_qconv2d_fwd instead. */
+int qnn_qconv2d_fwd_nchw_f32(const float* x, int c, int h, int w, int pad, float neg_min, float scale, float qmax,
+                             const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi, int tile,
+                             qnn_stream_t stream);
+
 /* Tile plan qnn_qconv2d_fwd would use for this layer (introspection for benchmarks and
  * profiles; no GPU work): configuration id, block tile (cout x pixels), and the number of
  * block tiles (the persistent direct-fragment grid loops over them: qnn_conv_occupancy.grid

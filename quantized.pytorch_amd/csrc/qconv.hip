@@ -1692,15 +1692,15 @@ extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue*
   return QNN_OK;
 }
 
-extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
-                               qnn_stream_t stream) {
+// the arguments of a forward launch (x: the code tensor, or the fp32 input of the _nchw_f32 entry);
+// QNN_OK with p filled, -1 for an empty batch (nothing to launch), else the error status
+static int fwd_args(const void* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi, Params& p) {
   QNN_REQUIRE(desc && epi, "null descriptor");
   const qnn_conv_desc& d = *desc;
   const qnn_epilogue& e = *epi;
-  Params p;
   const int rc0 = conv_params(d, e, p);
   if (rc0 != QNN_OK) return rc0;
-  if (d.n == 0) return QNN_OK;
+  if (d.n == 0) return -1;
   QNN_REQUIRE(x && wq && e.sxsw && e.sxbw && e.table && e.hcls && e.wcls, "null pointer");
   QNN_REQUIRE((((uintptr_t)x) & 15) == 0 && (((uintptr_t)wq) & 15) == 0, "x/wq must be 16-byte aligned");
   if (e.mode == 0) {
@@ -1730,11 +1730,56 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
                   "bad residual chain link (16-B aligned codes, RangeBN params, scale > 0)");
     }
   }
+  return QNN_OK;
+}
+
+extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv_desc* desc, const qnn_epilogue* epi,
+                               qnn_stream_t stream) {
+  Params p;
+  const int rc0 = fwd_args(x, wq, desc, epi, p);
+  if (rc0 != QNN_OK) return rc0 == -1 ? QNN_OK : rc0;
   hipStream_t s = (hipStream_t)stream;
   const int k = pick_cfg(p);
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   const int rc = launch_cfg(k, x, wq, p, s);
   if (rc != QNN_OK) return rc;
   QNN_LAUNCH_CHECK("qnn_qconv2d_fwd");
+  return QNN_OK;
+}
+
+// The drop-in forward from the module's fp32 NCHW input: one persistent-band launch quantizes the
+// input into its band buffers (quant_code_fast: bitwise the codes qnn_quantize_nchw_to_nhwc8 writes)
+// and convolves, instead of the quantize launch + qnn_qconv2d_fwd.  desc describes the code tensor
+// that quantize would write (hp = h + 2 pad, wp = w + 2 pad, cp >= c); tile: 0 for the cheapest
+// persistent-band configuration that fits, k + 1 for configuration k (45-49).  QNN_ERR_UNSUPPORTED when none does (the
+// caller then takes the two-launch path).
+extern "C" int qnn_qconv2d_fwd_nchw_f32(const float* x, int c, int h, int w, int pad, float neg_min, float scale,
+                                        float qmax, const int8_t* wq, const qnn_conv_desc* desc,
+                                        const qnn_epilogue* epi, int tile, qnn_stream_t stream) {
+  Params p;
+  const int rc0 = fwd_args(x, wq, desc, epi, p);
+  if (rc0 != QNN_OK) return rc0 == -1 ? QNN_OK : rc0;
+  const qnn_conv_desc& d = *desc;
+  QNN_REQUIRE(c >= 1 && c <= d.cp && h >= 1 && w >= 1 && pad >= 0 && d.hp == h + 2 * pad && d.wp == w + 2 * pad,
+              "fp32 input geometry must match the padded code tensor (hp = h + 2 pad, wp = w + 2 pad, c <= cp)");
+  QNN_REQUIRE(scale > 0.f && qmax >= 1.f && qmax <= 255.f, "bad input quantizer");
+  QNN_REQUIRE((int64_t)d.n * c * h * w < (1LL << 31), "input too large");
+  int k = -1;
+  if (tile > 0) {
+    QNN_REQUIRE(tile - 1 >= pb_first() && tile - 1 < ncfg_all(), "tile must be a persistent-band configuration");
+    if (pb_ok(tile - 1 - pb_first(), p)) k = tile - 1;
+  } else {
+    double best = 0;
+    for (int i = 0; i < pb_count(); ++i)
+      if (pb_ok(i, p) && (k < 0 || pb_cost(i, p) < best)) k = pb_first() + i, best = pb_cost(i, p);
+  }
+  if (k < 0) {
+    set_error("no persistent-band configuration for this layer (fp32 input)");
+    return QNN_ERR_UNSUPPORTED;
+  }
+  const F32In fin = {x, c, h, w, pad, neg_min, scale, qmax};
+  const int rc = pb_launch(k - pb_first(), nullptr, wq, p, (hipStream_t)stream, nullptr, &fin);
+  if (rc != QNN_OK) return rc;
+  QNN_LAUNCH_CHECK("qnn_qconv2d_fwd_nchw_f32");
   return QNN_OK;
 }

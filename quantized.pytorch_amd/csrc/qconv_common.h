@@ -186,7 +186,15 @@ void pb_tile(int k, int* bm, int* bn);
 bool pb_ok(int k, const Params& p);
 double pb_cost(int k, const Params& p);
 int64_t pb_blocks(int k, const Params& p);
-int pb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
+// qnn_qconv2d_fwd_nchw_f32: the drop-in's fp32 NCHW input and its quantizer (the persistent-band
+// kernel quantizes it into its band buffers instead of reading a code tensor)
+struct F32In {
+  const float* x;
+  int c, h, w, pad;
+  float neg_min, scale, qmax;
+};
+int pb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr,
+              const F32In* fin = nullptr);
 
 // stem_pool.hip: the space-to-depth stem conv fused with RangeBN's input codes and
 // MaxPool2d(3, 2, 1) (qnn_qconv2d_maxpool_fwd)

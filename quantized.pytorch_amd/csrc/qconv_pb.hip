@@ -79,6 +79,11 @@ struct Geo {
   int cls_off;    // LDS: hcls[ho] * nwc, then wcls[wo]
   int npt;        // 16-pixel tiles per band
   int lut;        // EK_LUT: the code table is staged (else evaluated)
+  // drop-in input as fp32 NCHW (qnn_qconv2d_fwd_nchw_f32): each wave quantizes its pixels of a band
+  // in registers (quant_code_fast, bitwise the IEEE quotient) into the band buffer, no code tensor
+  const float* xf;  // null: the input is the padded NHWC8 codes x
+  int fc, fh, fw, fpad;
+  float fnm, fs, fqmax;
   int wstage;     // stage the weights through LDS (else each wave loads them from L2)
   int wsep;       // ... in a region of their own at wst_off (else in the band buffers, wst_off = 0)
   int wst_off;
@@ -217,6 +222,8 @@ __device__ __forceinline__ void dma16v(const void* src, const int8_t* ldst) {
   const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
   asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
 }
+__device__ float qnn_pb_zero_page[64];  // zero-initialised: the bias vector of a bias-free layer, fp32 input
+
 template <class C, int EK>
 __device__ __forceinline__ void stage_epi_asm(const Params& p, const int8_t* x, int8_t* dst, int c0, int wave, int lane) {
   constexpr int BM = C::BM, W = C::W, CH = BM / 64;
@@ -234,8 +241,8 @@ __device__ __forceinline__ void stage_epi_asm(const Params& p, const int8_t* x, 
       case 0: src = e.sxsw; break;
       case 1: src = e.sxbw; break;
       case 2:
-        if (!e.bias) {  // no bias: zeros from the input's 128-byte zero page
-          src = reinterpret_cast<const float*>(x + p.d.zero_off);
+        if (!e.bias) {  // no bias: zeros from the input's 128-byte zero page (or the library's)
+          src = x ? reinterpret_cast<const float*>(x + p.d.zero_off) : qnn_pb_zero_page;
           c = lane & 31;
         } else {
           src = e.bias;
@@ -420,7 +427,7 @@ __device__ __forceinline__ void gen_epilogue(const Params& p, const v4i (&acc)[C
   }
 }
 
-template <class C, int EK, bool BIAS>
+template <class C, int EK, bool BIAS, bool F32 = false>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_pb_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
   constexpr int TM = C::TM, KS = C::KS, CB = C::CB, NT = C::NT;
@@ -459,8 +466,52 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     const int r0 = (bfirst + j * bstep) * g.rows;
     return (r0 / d.ho) * d.hp + (r0 % d.ho) * d.sh;
   };
+  auto fill_band_f32 = [&](int j) {  // this wave's pixels b = 64 (wave + W k) + lane of band j
+    int8_t* dst = smem + (j & 1) * g.buf;
+    const int R0 = band_row0(j);
+    const int rows_all = d.n * d.hp;
+    const float inv_wb = 1.0f / (float)g.wb, inv_hp = 1.0f / (float)d.hp;
+    const QParams qp = make_qparams(g.fnm, g.fs, g.fqmax);
+    const int plane_hw = g.fh * g.fw;
+    for (int b = 64 * wave + lane; b < g.nbp; b += 64 * C::W) {
+      int br, cc, n, hr;
+      fdivmod(b, g.wb, inv_wb, br, cc);
+      const int col = g.s2 ? (cc < g.we ? 2 * cc : 2 * (cc - g.we) + 1) : cc;
+      const int pr = R0 + br;
+      fdivmod(pr < rows_all ? pr : rows_all - 1, d.hp, inv_hp, n, hr);
+      const int ih = hr - g.fpad, iw = col - g.fpad;
+      const bool in = pr < rows_all && ih >= 0 && ih < g.fh && iw >= 0 && iw < g.fw;
+      const float* src = g.xf + ((int64_t)n * g.fc * g.fh + (in ? ih : 0)) * g.fw + (in ? iw : 0);
+      // 16 channels per step: their loads in flight together, one 16-byte LDS write (one step at a
+      // time: more in flight spills the resident weights)
+#pragma unroll 1
+      for (int k = 0; k < 4 * C::G; ++k) {
+        float f[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int ch = 16 * k + u;
+          f[u] = in && ch < g.fc ? src[ch * plane_hw] : 0.f;
+        }
+        unsigned wd[4];
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) {
+          unsigned x4 = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int ch = 16 * k + 4 * u4 + u;
+            const unsigned code = (unsigned)(int)quant_code_fast(f[4 * u4 + u], qp.nm, qp.s, qp.inv, qp.qmax) - 128u;
+            x4 |= ((in && ch < g.fc ? code : 0u) & 255u) << (8 * u);
+          }
+          wd[u4] = x4;
+        }
+        *reinterpret_cast<int4*>(dst + (k >> 1) * g.pl + 32 * b + 16 * (k & 1)) =
+            make_int4((int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]);
+      }
+    }
+  };
   auto issue_band = [&](int j) {
     if (QNN_ABLATE == 3) return;
+    if constexpr (F32) return fill_band_f32(j);
     const uint32_t base = (uint32_t)band_row0(j) * (uint32_t)(d.wp * d.cp);
     int8_t* dst = smem + (j & 1) * g.buf;
     int v = 0, r = wave;  // piece k = wave + W i = v * ppp + r
@@ -505,8 +556,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   // the older epilogue data and weights while the band pieces stay in flight
   const bool wlds = g.wstage && (g.wsep || 1024 * KS * TM <= 2 * g.buf);
   int issued = nb < 2 ? nb : 2, published = 0;
-  if (EK == EK_LUT && g.lut) stage_epi_asm<C, EK_LUT>(p, x, smem + p.epi_off, c0, wave, lane);
-  else stage_epi_asm<C, (EK == EK_LUT ? EK_BNCODE : EK)>(p, x, smem + p.epi_off, c0, wave, lane);
+  const int8_t* xz = F32 ? nullptr : x;  // the zero page's owner
+  if (EK == EK_LUT && g.lut) stage_epi_asm<C, EK_LUT>(p, xz, smem + p.epi_off, c0, wave, lane);
+  else stage_epi_asm<C, (EK == EK_LUT ? EK_BNCODE : EK)>(p, xz, smem + p.epi_off, c0, wave, lane);
   // the weights: K step s = (group s / 9, tap s % 9) is weight bytes tap * cp + 64 group of rows
   // c0 + 16 i + (lane & 15), K bytes 16 (lane >> 4)
   auto wsrc = [&](int s, int i) {
@@ -519,7 +571,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   int band_dma = 0;                    // band pieces this wave has in flight
   if (early) {
     for (int j = 0; j < issued; ++j) issue_band(j);
-    band_dma = issued * ((g.npieces - wave + C::W - 1) / C::W);
+    band_dma = F32 ? 0 : issued * ((g.npieces - wave + C::W - 1) / C::W);  // (fp32 fill: synchronous)
   }
 #if QNN_STAMP
   PB_TS(tp2);
@@ -822,9 +874,11 @@ static int blocks_per_cu(const void* kern, int nt, int lds) {
   return n;
 }
 
-template <class C, int EK, bool BIAS = false>
-static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  auto kern = qconv_pb_kernel<C, EK, BIAS>;
+// F32: the fp32-input instantiation (qnn_qconv2d_fwd_nchw_f32; its own register allocation, so the
+// band fill's registers never touch the code-input kernels')
+template <class C, int EK, bool BIAS = false, bool F32 = false>
+static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ, const F32In* fin) {
+  auto kern = qconv_pb_kernel<C, EK, BIAS, F32>;
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -837,6 +891,12 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
     return v ? atoi(v) : 1;
   }();
   g.wstage = wstage;
+  g.xf = nullptr;
+  if (fin) {
+    g.xf = fin->x;
+    g.fc = fin->c, g.fh = fin->h, g.fw = fin->w, g.fpad = fin->pad;
+    g.fnm = fin->neg_min, g.fs = fin->scale, g.fqmax = fin->qmax;
+  }
   const int nby = (int)cdiv(p.d.cout, C::CB);
   const int per_cu = blocks_per_cu((const void*)kern, C::NT, lds);
   int64_t nblk = ((int64_t)NUM_CU * per_cu / nby) * nby;
@@ -852,14 +912,19 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
 }
 
 template <class C>
-static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+static int launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ, const F32In* fin) {
+  if (fin) {  // the drop-in's fp32 input: built for its fp32 NCHW output only
+    if (epi_kind(p.e) != EK_NCHW) return arg_error("fp32-input convolution: fp32 NCHW output only");
+    return launch<C, EK_NCHW, false, true>(x, w, p, s, occ, fin);
+  }
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return launch<C, EK_NCHW>(x, w, p, s, occ);
-    case EK_LUT: return p.e.bias ? launch<C, EK_LUT, true>(x, w, p, s, occ) : launch<C, EK_LUT, false>(x, w, p, s, occ);
-    case EK_BNCODE: return launch<C, EK_BNCODE>(x, w, p, s, occ);
+    case EK_NCHW: return launch<C, EK_NCHW>(x, w, p, s, occ, fin);
+    case EK_LUT:
+      return p.e.bias ? launch<C, EK_LUT, true>(x, w, p, s, occ, fin) : launch<C, EK_LUT, false>(x, w, p, s, occ, fin);
+    case EK_BNCODE: return launch<C, EK_BNCODE>(x, w, p, s, occ, fin);
     default:  // the general chain beside 144 resident weight registers spills at two waves per SIMD: not built
       if constexpr (C::TM * C::KS > 18 && C::BPC * C::W / 4 > 1) return arg_error("tile configuration not built for this layer / epilogue kind");
-      else return launch<C, EK_GEN>(x, w, p, s, occ);
+      else return launch<C, EK_GEN>(x, w, p, s, occ, fin);
   }
 }
 
@@ -931,13 +996,13 @@ double pb_cost(int k, const Params& p) {
   return work / NUM_CU / f.rate;
 }
 
-int pb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+int pb_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ, const F32In* fin) {
   switch (k) {
-    case 0: return pb::launch_ek<pb::P0>(x, w, p, s, occ);
-    case 1: return pb::launch_ek<pb::P1>(x, w, p, s, occ);
-    case 2: return pb::launch_ek<pb::P2>(x, w, p, s, occ);
-    case 3: return pb::launch_ek<pb::P3>(x, w, p, s, occ);
-    case 4: return pb::launch_ek<pb::P4>(x, w, p, s, occ);
+    case 0: return pb::launch_ek<pb::P0>(x, w, p, s, occ, fin);
+    case 1: return pb::launch_ek<pb::P1>(x, w, p, s, occ, fin);
+    case 2: return pb::launch_ek<pb::P2>(x, w, p, s, occ, fin);
+    case 3: return pb::launch_ek<pb::P3>(x, w, p, s, occ, fin);
+    case 4: return pb::launch_ek<pb::P4>(x, w, p, s, occ, fin);
     default: return arg_error("tile configuration not built for this layer / epilogue kind");
   }
 }

@@ -86,20 +86,21 @@ __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementw
 #endif
 
 struct QParams {  // one per-tensor quantizer: x -> code
-  float nm, s, inv, lim, qmax;  // -min, scale, RN(1/scale), 2^20*scale, 2^bits-1
+  float nm, s, inv, qmax;  // -min, scale, RN(1/scale), 2^bits-1
 };
 
 __device__ __forceinline__ QParams make_qparams(float neg_min, float scale, float qmax) {
-  return {neg_min, scale, 1.0f / scale, 1048576.0f * scale, qmax};
+  return {neg_min, scale, 1.0f / scale, qmax};
 }
 
-// Clamped quotient clamp(RN((x + nm) / s), 0, qmax) of quant_code_fast for a pair, before
-// the final round.  The t clamp to +-2^20*s replaces quant_code_fast's |q0| < 2^20 select:
-// inside it the two are the same Markstein quotient, outside it both clamp to 0 / qmax.
+// Clamped quotient clamp(RN((x + nm) / s), 0, qmax) of quant_code_fast for a pair, before the
+// final round.  quant_code_fast's |q0| < 2^20 select is not needed here: inside that range the
+// two are the same Markstein quotient; beyond it the corrected quotient q differs from q0 by at
+// most a few ulps of q0 (|r| <= ulp(q0) s, x finite: every epilogue input is a finite fp32 sum of
+// finite codes times finite scales), so it is also beyond [0, qmax] on the same side and clamps to
+// the same 0 or qmax (tests/test_quant_math.py, clamp-free form vs IEEE division out to 2^31).
 __device__ __forceinline__ f2 qclamp2(f2 x, const QParams& p) {
-  f2 t = x + p.nm;
-  t.x = __builtin_amdgcn_fmed3f(t.x, -p.lim, p.lim);
-  t.y = __builtin_amdgcn_fmed3f(t.y, -p.lim, p.lim);
+  const f2 t = x + p.nm;
   const f2 inv = {p.inv, p.inv}, s = {p.s, p.s};
   const f2 q0 = t * inv;
   const f2 r = pfma(-q0, s, t);

@@ -153,6 +153,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   __syncthreads();
   const float* s_f = reinterpret_cast<const float*>(smem);
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+  const bool has_bias = e.bias != nullptr;
   float4 sw[TM], bw[TM], bi[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -242,10 +243,13 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         const v4i& a = acc[i];
         const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
         // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
-        const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
-                      (f2){bi[i].x, bi[i].y};
-        const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
-                      (f2){bi[i].z, bi[i].w};
+        f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y}));
+        f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w}));
+        if (has_bias) {  // (without one the other kernels add staged zeros: v + 0 differs from v only
+                         // for v = -0, and -0 and +0 quantize to the same code)
+          v0 = v0 + (f2){bi[i].x, bi[i].y};
+          v1 = v1 + (f2){bi[i].z, bi[i].w};
+        }
         const int kb = pack4(qclamp2(v0, bnp) + MAGIC_U8, qclamp2(v1, bnp) + MAGIC_U8);  // EK_BNCODE
         if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb ^ (int)dirw[i];
       }

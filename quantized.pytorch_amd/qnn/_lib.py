@@ -80,6 +80,8 @@ SIGNATURES = {
                            c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_conv_border_table": [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_float, c_ptr, c_ptr],
     "qnn_qconv2d_fwd": [c_ptr, c_ptr, ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr],
+    "qnn_qconv2d_fwd_nchw_f32": [c_ptr, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_ptr,
+                                 ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_int, c_ptr],
     "qnn_conv_plan": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_conv_occupancy": [ctypes.POINTER(ConvDesc), ctypes.POINTER(Epilogue), c_ptr, c_ptr, c_ptr, c_ptr],
     "qnn_dwconv2d_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -207,6 +209,32 @@ def call(name, *args):
     if rc != 0:
         msg = lib.qnn_last_error().decode(errors="replace")
         raise QnnError(f"{name} failed (status {rc}): {msg}")
+
+
+STATUS_UNSUPPORTED = 3  # QNN_ERR_UNSUPPORTED (include/qnn.h)
+
+
+def call_unsupported_ok(name, *args):
+    """call(), except that QNN_ERR_UNSUPPORTED is returned (False) instead of raised: for entry
+    points the caller has a fallback for.  True when the call ran."""
+    lib = load()
+    t = _timer
+    if t is not None and name in t.names:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib, name)(*args)
+        e1.record()
+        if rc == 0:
+            t.records.append((name, e0, e1))
+    else:
+        rc = getattr(lib, name)(*args)
+    if rc == STATUS_UNSUPPORTED:
+        return False
+    if rc != 0:
+        msg = lib.qnn_last_error().decode(errors="replace")
+        raise QnnError(f"{name} failed (status {rc}): {msg}")
+    return True
 
 
 def ptr(t):

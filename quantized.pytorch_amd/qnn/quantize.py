@@ -456,6 +456,12 @@ def s2d_kmask(kh, kw, cin_g, kpad, dev):
 # launches the library's cost-model choice.
 MODULE_AUTOTUNE = [os.environ.get("QNN_MODULE_AUTOTUNE", "0") == "1"]
 
+# QNN_FUSED_INPUT=1 (or FUSED_INPUT[0] = True; per layer: qnn_fused_input = True / False): a drop-in
+# 3x3 conv on 64 or 128 input channels quantizes its fp32 input inside the convolution
+# (qnn_qconv2d_fwd_nchw_f32, one launch) instead of a quantize launch + the conv.  Bitwise the same
+# output either way; DESIGN.md records the measured trade (profiles/r5_bench_layers_dropin.jsonl).
+FUSED_INPUT = [os.environ.get("QNN_FUSED_INPUT", "0") == "1"]
+
 
 class _QLayerMixin:
     """Shared int8 machinery of QConv2d / QLinear (QuantNode subclasses)."""
@@ -466,6 +472,9 @@ class _QLayerMixin:
         # configuration k (qnn_conv_plan); every configuration computes the identical result
         self.qnn_tile = 0
         self.qnn_keep_input = False
+        self.qnn_fused_input = None  # None: FUSED_INPUT[0]
+        self.qnn_fused_tile = 0      # its configuration: 0 = the cheapest that fits, k + 1 = k
+        self._last_fused = False     # whether the last forward took the one-launch path
 
     def _weight4(self):
         w = self.weight
@@ -652,9 +661,7 @@ class _QLayerMixin:
             d.kh, d.kw, d.sh, d.sw, d.cp = kh, kw, sh, sw, pk.cin_pad
             d.hp, d.wp = H + 2 * ph, W + 2 * pw
             nbytes = N * d.hp * d.wp * d.cp
-            xq = torch.empty(nbytes + 128, dtype=torch.int8, device=dev)
-            _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, ph, d.cp, -float(mn), s,
-                      qmax, st)
+            xq = None
         d.zero_off = nbytes
         d.kmask = None if pk.kmask is None else pk.kmask.data_ptr()
         d.tile = int(self.qnn_tile)
@@ -668,9 +675,24 @@ class _QLayerMixin:
         e.nwc, e.nclass = g[5], g[2] * g[5]
         e.bias = None if pk.qbias is None else pk.qbias.data_ptr()
         e.out_f32 = y.data_ptr()
+        if xq is None:
+            fused = self.qnn_fused_input if self.qnn_fused_input is not None else FUSED_INPUT[0]
+            # quantize-on-load: one launch reads the fp32 input (qnn_qconv2d_fwd_nchw_f32), when a
+            # persistent-band configuration fits the layer; else quantize, then convolve
+            if fused and pk.kmask is None and x4.is_contiguous() and _lib.call_unsupported_ok(
+                    "qnn_qconv2d_fwd_nchw_f32", _lib.ptr(x4), C, H, W, ph, -float(mn), s, qmax, _lib.ptr(pk.wq),
+                    ctypes.byref(d), ctypes.byref(e), int(self.qnn_fused_tile), st):
+                self._last_conv = (d, e)
+                self._last_xq = None
+                self._last_fused = True
+                return y
+            xq = torch.empty(nbytes + 128, dtype=torch.int8, device=dev)
+            _lib.call("qnn_quantize_nchw_to_nhwc8", _lib.ptr(x4), _lib.ptr(xq), N, C, H, W, ph, d.cp, -float(mn), s,
+                      qmax, st)
         if self.qnn_tile == 0 and MODULE_AUTOTUNE[0] and not torch.cuda.is_current_stream_capturing():
             d.tile = self._tuned_tile(xq, pk, d, e, st, (N, H, W, Ho, Wo))
         _lib.call("qnn_qconv2d_fwd", _lib.ptr(xq), _lib.ptr(pk.wq), ctypes.byref(d), ctypes.byref(e), st)
+        self._last_fused = False
         self._last_conv = (d, e)  # launch descriptors, for profiling tools (qnn_conv_plan)
         self._last_xq = xq if self.qnn_keep_input else None  # the codes, for tools that re-issue the launch
         return y

@@ -45,3 +45,46 @@ def test_markstein_quotient_is_ieee(tmp_path):
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
     out = subprocess.run([str(exe), "20000000"], check=True, capture_output=True, text=True).stdout
     assert int(out.strip()) == 0
+
+
+SRC_CLAMP = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+static uint64_t st = 0x243F6A8885A308D3ull;
+static inline uint64_t xr(void) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; }
+static inline float bits(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline float med3(float a, float lo, float hi) { return fminf(fmaxf(a, lo), hi); }
+int main(int argc, char** argv) {
+  long n = atol(argv[1]), bad = 0;
+  for (long it = 0; it < n; ++it) {
+    float s = bits((uint32_t)((xr() & 0x7fffff) | ((uint32_t)(100 + (int)(xr() % 36)) << 23)));
+    float inv = 1.0f / s;
+    /* quotients of magnitude 2^-2 .. 2^31, either sign, mantissa random */
+    float mag = ldexpf(1.0f + (float)(xr() >> 40) / 16777216.0f, (int)(xr() % 34) - 2);
+    float t = ((xr() & 1) ? mag : -mag) * s;
+    if (!isfinite(t)) continue;
+    float ref = rintf(med3(t / s, 0.0f, 255.0f));
+    float q0 = t * inv, q = fmaf(fmaf(-q0, s, t), inv, q0);
+    float fast = rintf(med3(q, 0.0f, 255.0f));
+    if (memcmp(&fast, &ref, 4)) ++bad;
+  }
+  printf("%ld\n", bad);
+  return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_clamp_free_quantizer_codes_are_ieee(tmp_path):
+    """qnn_internal.h qclamp2 without a clamp of x + nm before the Markstein quotient: the code
+    (quotient clamped to [0, 255], rounded half to even) equals the IEEE division's for every
+    finite quotient, including those far beyond 2^20 where q0 and the corrected q differ."""
+    c = tmp_path / "cf.c"
+    c.write_text(SRC_CLAMP)
+    exe = tmp_path / "cf"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
+    out = subprocess.run([str(exe), "20000000"], check=True, capture_output=True, text=True).stdout
+    assert int(out.strip()) == 0
