@@ -508,6 +508,72 @@ int qnn_grad_quant_f32(const float* g, const float* noise, float* out, int64_t n
   return QNN_OK;
 }
 
+// The same codes, 4 pixels per thread (w % 4 == 0, x 16-byte aligned): one float4 load per
+// channel (16 of them in flight: 64 values), 16 codes per pixel as one 16-byte store.  Lanes take
+// the cp / 16 channel groups fastest, so a store instruction's lanes write whole 64-128-byte
+// pixels, then the pixel quads along the row (a load instruction: cp / 16 planes x 256 B).  The
+// padding ring is written by the threads past the interior.  32-bit indices (checked by the host).
+__global__ __launch_bounds__(256) void quantize_nchw_nhwc8_q4_kernel(const float* __restrict__ x, int8_t* __restrict__ q,
+                                                                     int n, int c, int h, int w, int pad, int cp,
+                                                                     float neg_min, float scale, float qmax) {
+  const int hp = h + 2 * pad, wp = w + 2 * pad, G = cp >> 4, wq = w >> 2;
+  const int interior = n * h * wq * G;
+  const int ring = n * (hp * wp - h * w) * G;  // border pixels x groups
+  const float inv = 1.0f / scale;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < interior + ring; idx += gridDim.x * blockDim.x) {
+    if (idx < interior) {
+      const int g = idx % G, r = idx / G;
+      const int qd = r % wq, r2 = r / wq;
+      const int y = r2 % h, img = r2 / h;
+      const float* src = x + ((size_t)img * c * h + y) * w + 4 * qd;
+      const size_t hw = (size_t)h * w;
+      float4 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {  // channels past c re-read channel c - 1 (masked below): no
+        const int ch = min(16 * g + j, c - 1);  // per-load branch
+        v[j] = *reinterpret_cast<const float4*>(src + ch * hw);
+      }
+      int8_t* dst = q + (((size_t)img * hp + y + pad) * wp + pad + 4 * qd) * cp + 16 * g;
+#pragma unroll
+      for (int px = 0; px < 4; ++px) {
+        unsigned wd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          unsigned b = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = 4 * k + u;
+            const float f = px == 0 ? v[j].x : px == 1 ? v[j].y : px == 2 ? v[j].z : v[j].w;
+            const unsigned code = (unsigned)(int)quant_code_fast(f, neg_min, scale, inv, qmax) - 128u;
+            b |= ((16 * g + j < c ? code : 0u) & 255u) << (8 * u);
+          }
+          wd[k] = b;
+        }
+        *reinterpret_cast<int4*>(dst + px * cp) = make_int4((int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]);
+      }
+    } else {
+      // border pixel k of an image: the top pad rows, the bottom pad rows, then each interior row's
+      // left and right pad columns
+      const int k = idx - interior, g = k % G, r = k / G;
+      const int per_img = hp * wp - h * w, img = r / per_img, b = r % per_img;
+      const int top = pad * wp;
+      int y, col;
+      if (b < 2 * top) {
+        y = b < top ? b / wp : h + pad + (b - top) / wp;
+        col = (b < top ? b : b - top) % wp;
+      } else {
+        const int e = b - 2 * top, side = 2 * pad;
+        y = pad + e / side;
+        const int s = e % side;
+        col = s < pad ? s : w + s;
+      }
+      *reinterpret_cast<int4*>(q + (((size_t)img * hp + y) * wp + col) * cp + 16 * g) = make_int4(0, 0, 0, 0);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 8)  // 128-byte zero page after the tensor
+    *reinterpret_cast<int4*>(q + (size_t)n * hp * wp * cp + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
+}
+
 int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, int w, int pad, int cp,
                                float neg_min, float scale, float qmax, qnn_stream_t stream) {
   QNN_REQUIRE(n >= 0 && c > 0 && h > 0 && w > 0 && pad >= 0, "bad shape");
@@ -516,6 +582,13 @@ int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, i
   QNN_REQUIRE(q && (n == 0 || x), "null pointer");
   QNN_REQUIRE((((uintptr_t)q) & 15) == 0, "q must be 16-byte aligned");
   int64_t work = (int64_t)n * (h + 2 * pad) * (w + 2 * pad) * (cp / 16);
+  if (w % 4 == 0 && (((uintptr_t)x) & 15) == 0 && work < (1LL << 31) && (int64_t)n * c * h * w < (1LL << 31)) {
+    const int64_t t4 = (int64_t)n * h * (w / 4) * (cp / 16) + (int64_t)n * ((h + 2 * pad) * (w + 2 * pad) - h * w) * (cp / 16);
+    hipLaunchKernelGGL(quantize_nchw_nhwc8_q4_kernel, dim3(grid_for(t4 > 0 ? t4 : 1, 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, q, n, c, h, w, pad, cp, neg_min, scale, qmax);
+    QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_nhwc8");
+    return QNN_OK;
+  }
   hipLaunchKernelGGL(quantize_nchw_nhwc8_kernel, dim3(grid_for(work > 0 ? work : 1, 256)), dim3(256), 0,
                      (hipStream_t)stream, x, q, n, c, h, w, pad, cp, neg_min, scale, qmax);
   QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_nhwc8");

@@ -69,7 +69,11 @@ def test_fake_quant_tensor_and_none_kat(gpu):
         j += 1
 
 
-@pytest.mark.parametrize("shape,c_pad,pad", [((3, 24, 9, 11), 32, 1), ((2, 3, 33, 17), 16, 3), ((4, 64, 56, 56), 64, 0)])
+@pytest.mark.parametrize("shape,c_pad,pad", [
+    ((3, 24, 9, 11), 32, 1), ((2, 3, 33, 17), 16, 3),     # w % 4 != 0: one pixel per thread
+    ((4, 64, 56, 56), 64, 0), ((2, 40, 12, 16), 48, 1),   # w % 4 == 0: 4 pixels per thread + the padding ring
+    ((3, 24, 8, 20), 32, 2), ((2, 128, 28, 28), 128, 1), ((1, 5, 4, 4), 16, 3),
+])
 def test_activation_codes_padded_nhwc8(gpu, shape, c_pad, pad):
     N, C, H, W = shape
     x = synthetic.input_batch(shape, 5) * 2.0
