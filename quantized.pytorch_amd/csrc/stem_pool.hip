@@ -162,12 +162,19 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
     bw[i] = *reinterpret_cast<const float4*>(s_f + C + cl);
     bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * C + cl);
   }
+  // the stem codes, [stem pixel][64 bytes] with the channels of each pixel in LANE order: byte
+  // 16 g + 4 i + u is channel 16 i + 4 g + u, so a tile lane (4 g) stores its 16 codes as one
+  // conflict-free 16-byte write (channel order: 4-byte writes at a 64-byte pixel stride, 8-way
+  // bank conflicts); a pooling chunk cg then holds channels 16 k + 4 cg + u (k, u < 4)
   uint8_t* s_codes = reinterpret_cast<uint8_t*>(smem + pl.lds_codes);
-  // pool direction per channel: 0xff where relu o RangeBN is non-increasing (sq * wq < 0).  The
-  // tiles store their codes XOR the direction (the pooling's folded form), so the window
-  // reduction is a plain bytewise max and only its result is unfolded.
+  // pool direction per channel (the same lane order): 0xff where relu o RangeBN is non-increasing
+  // (sq * wq < 0).  The tiles store their codes XOR the direction (the pooling's folded form), so
+  // the window reduction is a plain bytewise max and only its result is unfolded.
   uint8_t* s_dir = reinterpret_cast<uint8_t*>(smem + pl.lds_dir);
-  if (tid < C) s_dir[tid] = (s_f[4 * C + tid] * s_f[5 * C + tid]) < 0.f ? 0xff : 0;
+  if (tid < C) {
+    const int ch = 16 * ((tid >> 2) & 3) + 4 * (tid >> 4) + (tid & 3);
+    s_dir[tid] = (s_f[4 * C + ch] * s_f[5 * C + ch]) < 0.f ? 0xff : 0;
+  }
   uint32_t dirw[TM];  // this lane's four channels of each row tile
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -229,13 +236,14 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         int z = sacc[0];
 #pragma unroll
         for (int i = 0; i < TM; ++i) z ^= acc[i][0] ^ acc[i][1] ^ acc[i][2] ^ acc[i][3];
-        if (t * 16 + (lane & 15) < q.npx) *reinterpret_cast<int*>(s_codes + (lr * d.wo + col) * C + 4 * g) = z;
+        if (t * 16 + (lane & 15) < q.npx) *reinterpret_cast<int*>(s_codes + (lr * d.wo + col) * C + 16 * g) = z;
         continue;
       }
       const int pc = s_hc[q.sr_lo + lr] + s_hc[d.ho + col];
       const f2 p2 = {(float)sacc[0], (float)sacc[0]};
       const bool ok = t * 16 + (lane & 15) < q.npx;
-      uint8_t* dst = s_codes + (lr * d.wo + col) * C + 4 * g;
+      uint8_t* dst = s_codes + (lr * d.wo + col) * C + 16 * g;
+      int kk[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int cl = 16 * i + 4 * g;
@@ -251,8 +259,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
           v1 = v1 + (f2){bi[i].z, bi[i].w};
         }
         const int kb = pack4(qclamp2(v0, bnp) + MAGIC_U8, qclamp2(v1, bnp) + MAGIC_U8);  // EK_BNCODE
-        if (ok) *reinterpret_cast<int*>(dst + 16 * i) = kb ^ (int)dirw[i];
+        kk[i] = kb ^ (int)dirw[i];
       }
+      if (ok) *reinterpret_cast<int4*>(dst) = make_int4(kk[0], kk[1], kk[2], kk[3]);
     }
     __syncthreads();
     // one band buffer: the tiles are done with it, the next item's band lands under the pooling
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
       if (pl.out_code) {
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          const int ch = cb + 4 * s4;
+          const int ch = 16 * s4 + 4 * cg;  // the chunk's dword s4: channels ch .. ch + 3
           *reinterpret_cast<uint32_t*>(pl.out_code + btile_off((int)(m >> 5), ch >> 5, ct, (int)(m & 31) + 32 * ((ch >> 2) & 1)) +
                                        4 * ((ch & 31) >> 3)) = qd[s4];
         }
@@ -311,18 +320,17 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         const qnn_code_out& co = o ? pl.c1 : pl.c0;
         if (!co.ptr) continue;
         const int8_t* sl = smem + (o ? pl.lds_lut1 : pl.lds_lut0);
-        int r4[4];
+        int8_t* op = co.ptr + (((int64_t)q.img * co.hp + oy + co.pad) * co.wp + pc + co.pad) * co.cp + 4 * cg;
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          r4[s4] = 0;
+          int r4 = 0;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int ch = cb + 4 * s4 + u;
-            r4[s4] |= ((int)(uint8_t)sl[ch * 256 + ((qd[s4] >> (8 * u)) & 255)]) << (8 * u);
+            const int ch = 16 * s4 + 4 * cg + u;
+            r4 |= ((int)(uint8_t)sl[ch * 256 + ((qd[s4] >> (8 * u)) & 255)]) << (8 * u);
           }
+          *reinterpret_cast<int*>(op + 16 * s4) = r4;
         }
-        *reinterpret_cast<int4*>(co.ptr + (((int64_t)q.img * co.hp + oy + co.pad) * co.wp + pc + co.pad) * co.cp + cb) =
-            make_int4(r4[0], r4[1], r4[2], r4[3]);
       }
     }
   }
