@@ -1435,6 +1435,17 @@ using B14 = Cfg<4, 2, 2, 2, 64, 3, 1>;
 using B15 = Cfg<1, 4, 2, 2, 64, 3, 2>;
 using B16 = Cfg<2, 2, 2, 2, 64, 3, 2>;
 using B17 = Cfg<1, 2, 2, 2, 64, 3, 4>;
+// ring-loop configurations after the persistent band (ids 50-53): deeper K stages (BK 128: half
+// the barriers per K) and smaller blocks (more resident blocks on the small-spatial deep-K
+// layers, ResNet layer 4's 392 tiles of 64 x 128 leave ~1.5 blocks per CU)
+//   50   64 x 128   4 waves (64 x 32)   BK 128, 3 x 24 KiB   2 blocks/CU
+//   51   64 x  64   2 waves (64 x 32)   BK 64,  3 x 8 KiB    4
+//   52   64 x 128   4 waves (32 x 64)   BK 64,  3 x 12 KiB   4
+//   53   64 x  64   2 waves (64 x 32)   BK 128, 3 x 16 KiB   2
+using X0 = Cfg<1, 4, 2, 1, 128, 3, 2>;
+using X1 = Cfg<1, 2, 2, 1, 64, 3, 4>;
+using X2 = Cfg<2, 2, 1, 2, 64, 3, 4>;
+using X3 = Cfg<1, 2, 2, 1, 128, 3, 2>;
 constexpr int NCFG = 18;  // qconv.hip configurations (9: C6 with 2 k-steps per phase); then qconv16.hip's
 struct CfgInfo {
   int bm, bn, per_cu, waves;
@@ -1450,16 +1461,23 @@ static const CfgInfo CFG[NCFG] = {
     {64, 256, 2, 4, 0.70f, true},   {128, 128, 2, 4, 0.67f, true},  {64, 128, 4, 2, 0.45f, true},
 };
 
+constexpr int NX = 4;
+static const CfgInfo XCFG[NX] = {
+    {64, 128, 2, 4, 0.40f, false}, {64, 64, 4, 2, 0.40f, false}, {64, 128, 4, 4, 0.40f, false}, {64, 64, 2, 2, 0.40f, false},
+};
+
 // Whether configuration k is built for (and fits) this layer and epilogue kind
-static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1 + pb_count(); }
+static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1 + pb_count() + NX; }
 static int rb_first() { return NCFG + q16_count(); }
 static int rbp_first() { return NCFG + q16_count() + rb_count(); }
 static int dtab_first() { return rbp_first() + rbp_count(); }
 static int dhead_id() { return dtab_first() + dtab_count(); }  // configuration 44: the classifier head
 static int pb_first() { return dhead_id() + 1; }                 // configurations 45-49: persistent band
+static int xr_first() { return pb_first() + pb_count(); }         // configurations 50-53: extra ring tiles
 
 static bool cfg_ok(int k, const Params& p) {
   if (k >= ncfg_all()) return false;
+  if (k >= xr_first()) return epi_kind(p.e) != EK_GEN || XCFG[k - xr_first()].bm * XCFG[k - xr_first()].bn < 65536;
   if (k >= pb_first()) return pb_ok(k - pb_first(), p);
   if (k == dhead_id()) return dhead_ok(p);
   if (k >= dtab_first()) return dtab_ok(k - dtab_first(), p);
@@ -1479,13 +1497,14 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
-  if (k >= pb_first()) return pb_cost(k - pb_first(), p);
+  const bool xr = k >= xr_first();  // the extra ring tiles: the ring's cost model below
+  if (!xr && k >= pb_first()) return pb_cost(k - pb_first(), p);
   if (k == dhead_id()) return p.M <= 256 ? 0.0 : 1e30;  // measured: ahead of cfg 11 at b128 (6.4 vs 11.2 us), behind at b512
-  if (k >= dtab_first()) return dtab_cost(k - dtab_first(), p);
-  if (k >= rbp_first()) return rbp_cost(k - rbp_first(), p);
-  if (k >= rb_first()) return rb_cost(k - rb_first(), p);
-  if (k >= NCFG) return q16_cost(k - NCFG, p);
-  const CfgInfo& c = CFG[k];
+  if (!xr && k >= dtab_first()) return dtab_cost(k - dtab_first(), p);
+  if (!xr && k >= rbp_first()) return rbp_cost(k - rbp_first(), p);
+  if (!xr && k >= rb_first()) return rb_cost(k - rb_first(), p);
+  if (!xr && k >= NCFG) return q16_cost(k - NCFG, p);
+  const CfgInfo& c = xr ? XCFG[k - xr_first()] : CFG[k];
   const int64_t tiles = cdiv(p.M, c.bn) * cdiv(p.d.cout, c.bm);
   const int64_t slots = (int64_t)NUM_CU * c.per_cu;
   const int64_t rounds = cdiv(tiles, slots);
@@ -1515,6 +1534,14 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (k >= xr_first()) {
+    switch (k - xr_first()) {
+      case 0: return launch_ek<X0>(x, w, p, s);
+      case 1: return launch_ek<X1>(x, w, p, s);
+      case 2: return launch_ek<X2>(x, w, p, s);
+      default: return launch_ek<X3>(x, w, p, s);
+    }
+  }
   if (k >= pb_first()) return pb_launch(k - pb_first(), x, w, p, s);
   if (k == dhead_id()) return dhead_launch(x, w, p, s);
   if (k >= dtab_first()) return dtab_launch(k - dtab_first(), x, w, p, s);
@@ -1597,6 +1624,7 @@ extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
 extern "C" const char* qnn_conv_tile_kernel(int k) {
   if (k < 0 || k >= ncfg_all()) return nullptr;
+  if (k >= xr_first()) return "qconv_kernel";
   if (k >= pb_first()) return "qconv_pb_kernel";
   if (k == dhead_id()) return "qconv_direct_kernel";
   if (k >= dtab_first()) return "qconv_dtab_kernel";
@@ -1618,7 +1646,8 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   int tbm, tbn;
-  if (k >= pb_first()) pb_tile(k - pb_first(), &tbm, &tbn);
+  if (k >= xr_first()) tbm = XCFG[k - xr_first()].bm, tbn = XCFG[k - xr_first()].bn;
+  else if (k >= pb_first()) pb_tile(k - pb_first(), &tbm, &tbn);
   else if (k == dhead_id()) tbm = 16, tbn = 64;
   else if (k >= dtab_first()) dtab_tile(k - dtab_first(), &tbm, &tbn);
   else if (k >= rbp_first()) rbp_tile(k - rbp_first(), &tbm, &tbn);
@@ -1628,7 +1657,8 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
   if (nblk)
-    *nblk = k >= pb_first() ? (int)pb_blocks(k - pb_first(), p)
+    *nblk = k >= xr_first() ? (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm))
+            : k >= pb_first() ? (int)pb_blocks(k - pb_first(), p)
             : k == dhead_id() ? (int)dhead_blocks(p)
             : k >= dtab_first() ? (int)dtab_blocks(k - dtab_first(), p)
             : k >= rbp_first() ? (int)rbp_blocks(k - rbp_first(), p)
@@ -1677,7 +1707,8 @@ extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue*
   if (rc != QNN_OK) return rc;
   const int k = pick_cfg(p);
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
-  QNN_REQUIRE(k >= rb_first(), "occupancy is reported for the resident-band and direct-fragment configurations");
+  QNN_REQUIRE(k >= rb_first() && k < xr_first(),
+              "occupancy is reported for the resident-band, direct-fragment and persistent-band configurations");
   Occ o{0, 0, 0};
   const int r = k >= pb_first()    ? pb_launch(k - pb_first(), nullptr, nullptr, p, nullptr, &o)
                 : k == dhead_id()    ? dhead_launch(nullptr, nullptr, p, nullptr, &o)

@@ -76,7 +76,7 @@ struct Pool {
   int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc, lds_band, lds_band_bytes, lds_zero;  // LDS offsets
 };
 
-template <int KS, bool MASKED>
+template <int KS, bool MASKED, bool BIAS>
 __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                        const Params p, const Pool pl) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -153,7 +153,6 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   __syncthreads();
   const float* s_f = reinterpret_cast<const float*>(smem);
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
-  const bool has_bias = e.bias != nullptr;
   float4 sw[TM], bw[TM], bi[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -253,8 +252,8 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
         f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y}));
         f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w}));
-        if (has_bias) {  // (without one the other kernels add staged zeros: v + 0 differs from v only
-                         // for v = -0, and -0 and +0 quantize to the same code)
+        if constexpr (BIAS) {  // (without one the other kernels add staged zeros: v + 0 differs from v
+                               // only for v = -0, and -0 and +0 quantize to the same code)
           v0 = v0 + (f2){bi[i].x, bi[i].y};
           v1 = v1 + (f2){bi[i].z, bi[i].w};
         }
@@ -336,9 +335,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   }
 }
 
-template <int KS, bool MASKED>
+template <int KS, bool MASKED, bool BIAS>
 static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool& pl0, hipStream_t s) {
-  auto kern = stem_pool_kernel<KS, MASKED>;
+  auto kern = stem_pool_kernel<KS, MASKED, BIAS>;
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -383,11 +382,18 @@ int stem_pool_launch(const int8_t* x, const int8_t* w, const Params& p, int pool
   pl.ho = pool_ho, pl.wo = pool_wo, pl.nrg = (pool_ho + PR - 1) / PR;
   pl.out_code = out_code, pl.lut0 = lut0, pl.c0 = c0, pl.lut1 = lut1, pl.c1 = c1;
   const bool m = d.kmask != nullptr;
+  // the bias as a template parameter: a run-time test inside the tile loop is if-converted into
+  // an add and a select per output
+  auto go = [&](auto ks) {
+    constexpr int K = decltype(ks)::value;
+    if (p.e.bias) return m ? launch<K, true, true>(x, w, p, pl, s) : launch<K, false, true>(x, w, p, pl, s);
+    return m ? launch<K, true, false>(x, w, p, pl, s) : launch<K, false, false>(x, w, p, pl, s);
+  };
   switch ((p.taps * (d.cp >> 4) + 3) >> 2) {
-    case 1: return m ? launch<1, true>(x, w, p, pl, s) : launch<1, false>(x, w, p, pl, s);
-    case 2: return m ? launch<2, true>(x, w, p, pl, s) : launch<2, false>(x, w, p, pl, s);
-    case 3: return m ? launch<3, true>(x, w, p, pl, s) : launch<3, false>(x, w, p, pl, s);
-    default: return m ? launch<4, true>(x, w, p, pl, s) : launch<4, false>(x, w, p, pl, s);
+    case 1: return go(std::integral_constant<int, 1>{});
+    case 2: return go(std::integral_constant<int, 2>{});
+    case 3: return go(std::integral_constant<int, 3>{});
+    default: return go(std::integral_constant<int, 4>{});
   }
 }
 

@@ -100,15 +100,17 @@ def test_tile_kernel_families(lib):
     # families are contiguous id ranges; round 4 appended the two-team resident band, then the
     # table-epilogue direct configurations (ids of earlier families never move)
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
-    # the ring family is split by the ping-pong ids 6-9, the direct family by ids 40-43 (the
-    # classifier head, 44, is a direct-fragment configuration appended in round 4)
-    assert len(runs) == len(set(runs)) + 2
+    # the ring family is split by the ping-pong ids 6-9 and again by ids 12-49 (round 5 appended
+    # ring configurations 50-53), the direct family by ids 40-43 (the classifier head, 44, is a
+    # direct-fragment configuration appended in round 4)
+    assert len(runs) == len(set(runs)) + 3
     assert len(_lib.tile_ids("qconv_direct_kernel")) == 6 and _lib.tile_ids("qconv_direct_kernel")[-1] == 44
     assert _lib.tile_ids("qconv_rbp_kernel") == [40, 41]
     assert _lib.tile_ids("qconv_dtab_kernel") == [42, 43]
     assert fams[44] == "qconv_direct_kernel"
     # round 5 appended the persistent-band configurations 45-49
-    assert _lib.tile_ids("qconv_pb_kernel") == [45, 46, 47, 48, 49] and len(fams) == 50
+    assert _lib.tile_ids("qconv_pb_kernel") == [45, 46, 47, 48, 49]
+    assert [fams[k] for k in range(50, 54)] == ["qconv_kernel"] * 4 and len(fams) == 54
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 
@@ -152,3 +154,35 @@ def test_built_for_gfx950_only():
     blob = open(LIB, "rb").read()
     assert b"gfx950" in blob
     assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_conv_plan_every_configuration_host_only(lib):
+    """qnn_conv_plan (host code only: configuration filters and the cost model) for the benched
+    layer shapes, with the cost-model choice and with every configuration forced: returns a
+    configuration or refuses it with a message, never crashes (a cost-model table indexed past its
+    family's end once divided by zero here)."""
+    import ctypes
+    from qnn import _lib
+    shapes = [  # (n, cin_pad, cout, k, stride, hw)
+        (128, 64, 64, 3, 1, 56), (128, 512, 512, 3, 1, 7), (256, 256, 256, 3, 1, 14), (256, 64, 256, 1, 1, 56),
+        (128, 256, 512, 1, 2, 14), (37, 2048, 1000, 1, 1, 1)]
+    for n, cp, cout, k, st, hw in shapes:
+        pad = k // 2
+        ho = (hw + 2 * pad - k) // st + 1
+        kpad = -(-k * k * cp // 128) * 128
+        d = _lib.ConvDesc(n=n, hp=hw + 2 * pad, wp=hw + 2 * pad, cp=cp, zero_off=0, cout=cout, cout_pad=cout, kh=k,
+                          kw=k, sh=st, sw=st, ho=ho, wo=ho, kpad=kpad)
+        for mode in (0, 1):
+            e = _lib.Epilogue(mode=mode, nwc=1, nclass=1)
+            cfg, bm, bn, nb = (ctypes.c_int() for _ in range(4))
+            for tile in range(_lib.CONV_TILES + 1):
+                d.tile = tile
+                rc = lib.qnn_conv_plan(ctypes.byref(d), ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(bm),
+                                       ctypes.byref(bn), ctypes.byref(nb))
+                if tile == 0:
+                    assert rc == 0 and 0 <= cfg.value < _lib.CONV_TILES
+                if rc == 0:
+                    assert bm.value > 0 and bn.value > 0 and nb.value > 0
+                    assert tile == 0 or cfg.value == tile - 1
+                else:
+                    assert lib.qnn_last_error()
