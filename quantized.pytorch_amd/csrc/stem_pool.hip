@@ -25,6 +25,23 @@
 #include "qconv_common.h"
 #include "epi16.h"
 
+#ifndef QNN_STAMP
+#define QNN_STAMP 0  // diagnostic builds only (make spstamp): per-wave s_memtime phase sums
+#endif
+#if QNN_STAMP
+// [block][wave][8]: realtime start/end (100 MHz); cycles: prologue, item tops (band wait +
+// barrier), tiles, mid barrier, pooling; items
+__device__ unsigned long long qnn_sp_stamps[1 << 16];
+#define SP_TS(v)                                                                          \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+#else
+#define SP_TS(v) ((void)0)
+#endif
+
 #ifndef QNN_SP_ABLATE
 #define QNN_SP_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no tile epilogue, 3 no pooling, 4 no band DMA
 #endif
@@ -64,6 +81,21 @@ __device__ __forceinline__ void fdivmod(int m, int D, float invD, int& q, int& r
   if (r < 0) --q, r += D;
   if (r >= D) ++q, r -= D;
 }
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to 63: vector memory operations
+// complete in issue order, so at most n younger ones in flight still means every older one is done)
+template <int N = 0>
+__device__ __forceinline__ void wait_vmcnt_upto(int n) {
+  if constexpr (N < 63) {
+    if (n <= N) {
+      wait_vmcnt<N>();
+      return;
+    }
+    wait_vmcnt_upto<N + 1>(n);
+  } else {
+    wait_vmcnt<63>();
+  }
+}
+
 struct Pool {
   int ho, wo;            // pooled output
   int nrg;               // row groups per image (ceil(ho / PR))
@@ -119,6 +151,11 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   };
   int it = blockIdx.x;
   if (it >= pl.nitems) return;
+#if QNN_STAMP
+  unsigned long long t0 = 0, ta = 0, tb = 0, c_pro = 0, c_top = 0, c_tile = 0, c_mid = 0, c_pool = 0, nit = 0;
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+  SP_TS(t0);
+#endif
   issue_band(item(it), 0);
   // ---- staged once: epilogue vectors + border table (stage_epi), code tables, border classes
   stage_epi<Cfg, EK_BNCODE>(p, x, smem, 0, wave, lane);
@@ -187,13 +224,32 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   const float inv_wo = 1.0f / (float)d.wo, inv_pwo = 1.0f / (float)pl.wo;
   const int ct = (C + 31) >> 5;
 
+  // global stores the wave issued since the current item's band DMA (the previous item's pooled
+  // codes): the band is waited for with those left in flight
+  int nst = 0;
+  const int st_per = (pl.out_code ? 4 : 0) + (pl.c0.ptr ? 4 : 0) + (pl.c1.ptr ? 4 : 0);
+#if QNN_STAMP
+  SP_TS(ta);
+  c_pro = ta - t0;
+#endif
   for (int buf = 0; it < pl.nitems; it += gridDim.x, buf ^= (DB ? 1 : 0)) {
     const Item q = item(it);
+#if QNN_STAMP
+    SP_TS(ta);
+    ++nit;
+#endif
     // this item's band landed (every wave's pieces) and the previous item's pooling is done
     // with the codes: then the next item's band DMA goes into the other buffer, whose last
-    // reader (the previous item's tiles) finished before the previous barrier
-    wait_vmcnt<0>();
-    __syncthreads();
+    // reader (the previous item's tiles) finished before the previous barrier.  A raw barrier
+    // (__syncthreads would also wait for the pooled-code stores)
+    wait_vmcnt_upto(__builtin_amdgcn_readfirstlane(nst));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    nst = 0;
+#if QNN_STAMP
+    SP_TS(tb);
+    c_top += tb - ta;
+    ta = tb;
+#endif
     if (DB && it + (int)gridDim.x < pl.nitems) issue_band(item(it + gridDim.x), buf ^ 1);
     const int band = pl.lds_band + buf * pl.lds_band_bytes;
     auto load_b = [&](int t, v4i (&fb)[KS], int& lr, int& col) {
@@ -206,48 +262,47 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         fb[s] = *reinterpret_cast<const v4i*>(smem + (doff[s] >= 0 ? base + doff[s] : pl.lds_zero));
     };
 
-    // ---- 1. stem tiles: wave w takes tiles w, w + W, ...; the next tile's fragments are read
-    //         from the band before this one's MFMAs
-    v4i fnx[KS];
-    int nlr = 0, ncol = 0;
-    if (wave < q.ntile) load_b(wave, fnx, nlr, ncol);
-    for (int t = wave; t < q.ntile; t += W) {
-      v4i fb[KS];
+    // ---- 1. stem tiles: wave w takes tiles w, w + W, ...  Software-pipelined: tile t + W's
+    //         MFMAs are issued before tile t's epilogue (two accumulator sets), so the matrix pipe
+    //         runs under the epilogue's VALU work instead of between epilogues; each tile's
+    //         fragments are read from the band a tile earlier still.
+    struct Acc {
+      v4i a[TM], s;
+    };
+    auto mfmas = [&](const v4i (&fb)[KS], Acc& A) {
+      A.s = (v4i){0, 0, 0, 0};
 #pragma unroll
-      for (int s = 0; s < KS; ++s) fb[s] = fnx[s];
-      const int lr = nlr, col = ncol;
-      if (t + W < q.ntile) load_b(t + W, fnx, nlr, ncol);
-      v4i acc[TM], sacc = (v4i){0, 0, 0, 0};
-#pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i] = (v4i){0, 0, 0, 0};
+      for (int i = 0; i < TM; ++i) A.a[i] = (v4i){0, 0, 0, 0};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (QNN_SP_ABLATE == 1) {
           asm volatile("" ::"v"(fb[s]));
-          sacc[0] += fb[s][0];
+          A.s[0] += fb[s][0];
           continue;
         }
-        sacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], sacc, 0, 0, 0);
+        A.s = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], A.s, 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], acc[i], 0, 0, 0);
+        for (int i = 0; i < TM; ++i) A.a[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], A.a[i], 0, 0, 0);
       }
-      if (QNN_SP_ABLATE == 2) {
-        int z = sacc[0];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) z ^= acc[i][0] ^ acc[i][1] ^ acc[i][2] ^ acc[i][3];
-        if (t * 16 + (lane & 15) < q.npx) *reinterpret_cast<int*>(s_codes + (lr * d.wo + col) * C + 16 * g) = z;
-        continue;
-      }
-      const int pc = s_hc[q.sr_lo + lr] + s_hc[d.ho + col];
-      const f2 p2 = {(float)sacc[0], (float)sacc[0]};
+    };
+    auto epilogue = [&](int t, int lr, int col, const Acc& A) {
       const bool ok = t * 16 + (lane & 15) < q.npx;
       uint8_t* dst = s_codes + (lr * d.wo + col) * C + 16 * g;
+      if (QNN_SP_ABLATE == 2) {
+        int z = A.s[0];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) z ^= A.a[i][0] ^ A.a[i][1] ^ A.a[i][2] ^ A.a[i][3];
+        if (ok) *reinterpret_cast<int*>(dst) = z;
+        return;
+      }
+      const int pc = s_hc[q.sr_lo + lr] + s_hc[d.ho + col];
+      const f2 p2 = {(float)A.s[0], (float)A.s[0]};
       int kk[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int cl = 16 * i + 4 * g;
         const float4 tb = *reinterpret_cast<const float4*>(s_f + (7 + pc) * C + cl);
-        const v4i& a = acc[i];
+        const v4i& a = A.a[i];
         const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
         // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
         f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y}));
@@ -261,8 +316,53 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         kk[i] = kb ^ (int)dirw[i];
       }
       if (ok) *reinterpret_cast<int4*>(dst) = make_int4(kk[0], kk[1], kk[2], kk[3]);
+    };
+    // one tile's MFMAs interleaved with the previous tile's epilogue: 1 MFMA per 8 VALU
+    auto interleave = [] {
+#pragma unroll
+      for (int k = 0; k < 5 * KS; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);  // VALU
+      }
+    };
+    Acc A0, A1;
+    v4i fnx[KS];
+    int t = wave, nlr = 0, ncol = 0, lrA = 0, colA = 0, lrB = 0, colB = 0;
+    if (t < q.ntile) {
+      load_b(t, fnx, lrA, colA);
+      mfmas(fnx, A0);
+      load_b(t + W, fnx, nlr, ncol);  // (past the last tile: clamped reads, results discarded)
     }
-    __syncthreads();
+    // unrolled by two: each accumulator set keeps its registers.  Branch-free steps (the next
+    // tile's MFMAs and fragment reads run even past the last tile, on clamped pixels, and are
+    // discarded), so the scheduler can interleave them with the epilogue.
+    while (t < q.ntile) {
+      mfmas(fnx, A1);
+      lrB = nlr, colB = ncol;
+      load_b(t + 2 * W, fnx, nlr, ncol);
+      epilogue(t, lrA, colA, A0);
+      interleave();
+      t += W;
+      if (t >= q.ntile) break;
+      mfmas(fnx, A0);
+      lrA = nlr, colA = ncol;
+      load_b(t + 2 * W, fnx, nlr, ncol);
+      epilogue(t, lrB, colB, A1);
+      interleave();
+      t += W;
+    }
+#if QNN_STAMP
+    SP_TS(tb);
+    c_tile += tb - ta;
+    ta = tb;
+#endif
+    // the codes are in LDS (raw barrier: the next item's band DMA stays in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#if QNN_STAMP
+    SP_TS(tb);
+    c_mid += tb - ta;
+    ta = tb;
+#endif
     // one band buffer: the tiles are done with it, the next item's band lands under the pooling
     if (!DB && it + (int)gridDim.x < pl.nitems) issue_band(item(it + gridDim.x), 0);
 
@@ -306,6 +406,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
       best.w = __builtin_bit_cast(uint32_t, lo[3]) | (__builtin_bit_cast(uint32_t, hi[3]) << 8);
       const uint32_t qd[4] = {best.x ^ dm.x, best.y ^ dm.y, best.z ^ dm.z, best.w ^ dm.w};
       const int64_t m = ((int64_t)q.img * pl.ho + oy) * pl.wo + pc;
+      nst += st_per;
       if (pl.out_code) {
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
@@ -332,7 +433,18 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         }
       }
     }
+#if QNN_STAMP
+    SP_TS(tb);
+    c_pool += tb - ta;
+#endif
   }
+#if QNN_STAMP
+  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && blockIdx.x < (1 << 16) / (8 * W)) {
+    unsigned long long* o = qnn_sp_stamps + ((size_t)blockIdx.x * W + wave) * 8;
+    o[0] = rt0, o[1] = rt1, o[2] = c_pro, o[3] = c_top, o[4] = c_tile, o[5] = c_mid, o[6] = c_pool, o[7] = nit;
+  }
+#endif
 }
 
 template <int KS, bool MASKED, bool BIAS>
@@ -368,6 +480,13 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool&
 }
 
 }  // namespace sp
+
+#if QNN_STAMP
+extern "C" int qnn_debug_stamps_sp(void* dst, size_t bytes) {
+  if (bytes > sizeof(::qnn_sp_stamps)) bytes = sizeof(::qnn_sp_stamps);
+  return hip_check(hipMemcpyFromSymbol(dst, HIP_SYMBOL(::qnn_sp_stamps), bytes), "stamps");
+}
+#endif
 
 int stem_pool_launch(const int8_t* x, const int8_t* w, const Params& p, int pool_ho, int pool_wo, uint8_t* out_code,
                      const int8_t* lut0, const qnn_code_out& c0, const int8_t* lut1, const qnn_code_out& c1,
