@@ -213,8 +213,9 @@ def in_graph_times(engine, reps):
     quantizer, pooling, depthwise ...), so the L2 / Infinity-Cache contents a launch meets are
     not exactly those of the full graph.
 
-    The contractions' time is the full forward's graph minus the graph of every other launch
-    kind (`conv_ms`): where the other kinds are a large share of the forward (MobileNet's
+    The contractions' time is the full forward's graph (the engine's own hipGraph, with each
+    residual block's downsample conv concurrent with the main path) minus the graph of every
+    other launch kind (`conv_ms`): where the other kinds are a large share of the forward (MobileNet's
     depthwise convs feed every pointwise conv through L2), the contraction-only graph reads
     those inputs from HBM instead and runs ~9 % slower than the same launches in the full
     graph; the difference keeps them in their place.  It includes the contractions' in-graph
@@ -227,7 +228,17 @@ def in_graph_times(engine, reps):
     conv_alone = _graph_ms(engine, conv_names, reps)
     if not other:
         return out, conv_alone, conv_alone
-    full = _graph_ms(engine, list(out), reps)
+    if engine.graph is not None:  # the forward itself (its residual-branch forks included)
+        engine.graph.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            engine.graph.replay()
+        e1.record()
+        e1.synchronize()
+        full = e0.elapsed_time(e1) / reps
+    else:
+        full = _graph_ms(engine, list(out), reps)
     rest = _graph_ms(engine, other, reps)
     return out, full - rest, conv_alone
 

@@ -69,20 +69,25 @@ __device__ unsigned long long qnn_dbg_epi[1 << 18];  // [block][wave][4]: stagin
 
 
 // Tile configuration: WGM x WGN waves, each (32*TM) x (32*TN) (cout x pixels), K stage
-// BK bytes, NS-slot LDS ring.
-template <int WGM_, int WGN_, int TM_, int TN_, int BK_, int NS_, int BPC_ = (WGM_ * WGN_ == 4 ? 2 : 1)>
+// BK bytes, NS-slot LDS ring.  KSP > 1 (the ring kernel only): KSP such wave grids in one block,
+// K group g taking stages g, g + KSP, ... through a ring of its own; the groups' accumulators
+// are summed through LDS before one group's epilogue (more waves on a tile without a global
+// split-K hand-off: the deep-K layers whose tiles leave CUs half empty).
+template <int WGM_, int WGN_, int TM_, int TN_, int BK_, int NS_, int BPC_ = (WGM_ * WGN_ == 4 ? 2 : 1), int KSP_ = 1>
 struct Cfg {
-  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, BK = BK_, NS = NS_;
-  static constexpr int W = WGM * WGN, NT = 64 * W;
+  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, BK = BK_, NS = NS_, KSP = KSP_;
+  static constexpr int WG = WGM * WGN;  // waves of one K group (the tile's wave grid)
+  static constexpr int W = WG * KSP, NT = 64 * W;
   static constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32;
   static constexpr int CPR = BK / 16;    // 16-B chunks per LDS row
   static constexpr int RPI = 1024 / BK;  // rows per 1 KiB LDS-DMA wave-instruction
-  static constexpr int NA = BM / RPI / W, NB = BN / RPI / W;  // DMA per wave per stage
+  static constexpr int NA = BM / RPI / WG, NB = BN / RPI / WG;  // DMA per wave per stage
   static constexpr int STAGE = (BM + BN) * BK;
   static constexpr int KS = BK / 32;  // MFMA k-steps per stage
   static constexpr int P = NA + NB;
   static constexpr int BPC = BPC_;  // resident blocks per CU the LDS budget must allow
-  static_assert((BM / RPI) % W == 0 && (BN / RPI) % W == 0, "DMA rows must split evenly over the waves");
+  static_assert((BM / RPI) % WG == 0 && (BN / RPI) % WG == 0, "DMA rows must split evenly over the waves");
+  static_assert(KSP == 1 || KSP == 2, "K groups");
   static_assert(BK == 64 || BK == 128, "BK");
   static_assert(NS >= 3 && NS <= 4, "ring depth");
 };
@@ -449,16 +454,19 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
                                                       const Params p) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NS = C::NS, W = C::W, TM = C::TM, TN = C::TN;
   constexpr int CPR = C::CPR, RPI = C::RPI, NA = C::NA, NB = C::NB, STAGE = C::STAGE, KS = C::KS, P = C::P;
+  constexpr int WG = C::WG, KSP = C::KSP;
   static_assert(!MASKED || TAPM == TAP_LDS, "masked (space-to-depth) stems use the LDS tap table");
   // one dynamic LDS object (a second __shared__ array can make hipcc drain vmcnt before ds_reads)
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  int* s_tap = reinterpret_cast<int*>(smem + NS * STAGE);
-  int8_t* s_mask = smem + NS * STAGE + 4 * MAX_TAPS;
+  int* s_tap = reinterpret_cast<int*>(smem + KSP * NS * STAGE);
+  int8_t* s_mask = smem + KSP * NS * STAGE + 4 * MAX_TAPS;
 
   const qnn_conv_desc& d = p.d;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  // K group kg (its own ring at kg * NS * STAGE) and the wave's place wg in the tile's wave grid
+  const int kg = wave / WG, wg = wave - kg * WG;
+  const int wm = wg / C::WGN, wn = wg % C::WGN;
 
   // ---- XCD-aware, bijective block -> tile map: each XCD gets a contiguous run of
   // tiles, output-channel tiles fastest so blocks sharing an activation tile share L2
@@ -490,7 +498,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   int bdelta[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int row = RPI * (wave + W * j) + lane / CPR;
+    const int row = RPI * (wg + WG * j) + lane / CPR;
     int m = m0 + row;
     if (m > p.M - 1) m = p.M - 1;
     const int n = m / HoWo, rem = m - n * HoWo, ho = rem / d.wo, wo = rem - ho * d.wo;
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   uint32_t aoff[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int row = RPI * (wave + W * j) + lane / CPR;
+    const int row = RPI * (wg + WG * j) + lane / CPR;
     const int crow = (c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0);  // never past the packed rows
     aoff[j] = (uint32_t)(crow * d.kpad + (swz<BK>(row, lane % CPR) - row * BK));
   }
@@ -511,15 +519,18 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   if (p.epi_early) stage_epi<C, EK>(p, x, smem + p.epi_off, c0, wave, lane);  // oldest DMAs: land under the loop
   if constexpr (TAPM == TAP_LDS || MASKED) __syncthreads();  // s_tap / s_mask
 
-  auto issue = [&](int st, int slot) {
+  int8_t* const ring = smem + kg * NS * STAGE;  // this K group's ring
+  // local stage ls of this K group = K stage kg + KSP ls
+  auto issue = [&](int ls, int slot) {
     if (QNN_ABLATE == 1) return;
-    int8_t* sa = smem + slot * STAGE;
+    const int st = kg + KSP * ls;
+    int8_t* sa = ring + slot * STAGE;
     int8_t* sb = sa + BM * BK;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       uint32_t off = aoff[j] + (uint32_t)(st * BK);
       asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(sa + (wave + W * j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(wblk + off), (lds_ptr_t)(sa + (wg + WG * j) * 1024), 16, 0, 0);
     }
     const int t0 = (st * CPR) >> p.lgcpt;                           // first tap of this stage
     const uint32_t uin = (uint32_t)(((st * CPR) & cpt_mask) << 4);  // chunk-in-tap part (cp > 16*CPR)
@@ -547,7 +558,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
         off = tap < p.taps ? bbase[j] + uin + to : zoff;
       }
       asm volatile("" : "+v"(off));  // keep ONE per-lane-address load (no saddr/vaddr branch split)
-      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wave + W * j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(x + off), (lds_ptr_t)(sb + (wg + WG * j) * 1024), 16, 0, 0);
     }
   };
 
@@ -570,14 +581,15 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     offb[ks] = BM * BK + (wn * 32 * TN + frow) * BK + xo;
   }
 
-  auto compute = [&](auto slotc, int st) {
+  auto compute = [&](auto slotc, int ls) {
     constexpr int BO = decltype(slotc)::value * STAGE;
+    const int st = kg + KSP * ls;
     v4i fa[2][TM], fb[2][TN];
     auto load = [&](int ks, int sl) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[sl][i] = *reinterpret_cast<const v4i*>(smem + BO + offa[ks] + i * 32 * BK);
+      for (int i = 0; i < TM; ++i) fa[sl][i] = *reinterpret_cast<const v4i*>(ring + BO + offa[ks] + i * 32 * BK);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[sl][j] = *reinterpret_cast<const v4i*>(smem + BO + offb[ks] + j * 32 * BK);
+      for (int j = 0; j < TN; ++j) fb[sl][j] = *reinterpret_cast<const v4i*>(ring + BO + offb[ks] + j * 32 * BK);
     };
     load(0, 0);
 #pragma unroll
@@ -607,7 +619,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     }
   };
 
-  const int nstage = d.kpad / BK;
+  const int nstage = d.kpad / BK / KSP;  // this K group's stages (the host checks KSP divides them)
   const bool late = p.stagger && wave >= 4;
 #if QNN_STAMP
   unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, c_iss = 0, c_wait = 0, c_comp = 0;
@@ -664,6 +676,34 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
 #pragma unroll
   for (int j = 0; j < TN; ++j) sumq[j] += __shfl_xor(sumq[j], 32, 64);
   __syncthreads();  // main-loop LDS is reused by the epilogue
+  if constexpr (KSP > 1) {
+    // K group 1's partial sums to group 0 through the free rings: per wave of the grid, its
+    // (TM TN 16 + TN) ints lane-linear (conflict-free), then group 0 adds them
+    constexpr int NR = TM * TN * 16 + TN;
+    int* red = reinterpret_cast<int*>(smem) + wg * NR * 64 + lane;
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[((i * TN + j) * 16 + r) * 64] = acc[i][j][r];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) red[(TM * TN * 16 + j) * 64] = sumq[j];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += red[((i * TN + j) * 16 + r) * 64];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sumq[j] += red[(TM * TN * 16 + j) * 64];
+    }
+    __syncthreads();  // the epilogue's LDS (staging, scratch) may overlap the hand-off area
+  }
   if (QNN_ABLATE == 3) {
     int z = sumq[0];
 #pragma unroll
@@ -683,6 +723,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     wait_vmcnt<0>();
     __syncthreads();
   }
+  if (KSP > 1 && kg != 0) return;  // group 0 runs the epilogue (no barrier follows)
   epilogue<C, EK>(p, acc, sumq, pcls, smem, m0, c0, wm, wn, lane, tid, wave);
 #if QNN_STAMP
   QNN_TS(ts1);
@@ -1260,7 +1301,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
 
 template <class C>
 static int main_lds_bytes(int tapm, bool masked) {
-  return C::NS * C::STAGE + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
+  const int red = C::KSP > 1 ? (C::TM * C::TN * 16 + C::TN) * 64 * 4 * C::WG : 0;  // K-group hand-off
+  const int ring = C::KSP * C::NS * C::STAGE;
+  return (ring > red ? ring : red) + ((tapm == TAP_LDS) ? 4 * MAX_TAPS : 0) + (masked ? MAX_MASK : 0);
 }
 
 // LDS of a launch: main loop (lds_main bytes at 0), epilogue data (early: beside the main
@@ -1442,10 +1485,14 @@ using B17 = Cfg<1, 2, 2, 2, 64, 3, 4>;
 //   51   64 x  64   2 waves (64 x 32)   BK 64,  3 x 8 KiB    4
 //   52   64 x 128   4 waves (32 x 64)   BK 64,  3 x 12 KiB   4
 //   53   64 x  64   2 waves (64 x 32)   BK 128, 3 x 16 KiB   2
+//   54   64 x 128   8 waves: 2 K groups x 4 (64 x 32), BK 64, 2 x 3 x 12 KiB   2   (even stage count)
+//   55   64 x 128   8 waves: 2 K groups x 4 (64 x 32), BK 128, 2 x 3 x 24 KiB  1   (even stage count)
 using X0 = Cfg<1, 4, 2, 1, 128, 3, 2>;
 using X1 = Cfg<1, 2, 2, 1, 64, 3, 4>;
 using X2 = Cfg<2, 2, 1, 2, 64, 3, 4>;
 using X3 = Cfg<1, 2, 2, 1, 128, 3, 2>;
+using X4 = Cfg<1, 4, 2, 1, 64, 3, 2, 2>;
+using X5 = Cfg<1, 4, 2, 1, 128, 3, 1, 2>;
 constexpr int NCFG = 18;  // qconv.hip configurations (9: C6 with 2 k-steps per phase); then qconv16.hip's
 struct CfgInfo {
   int bm, bn, per_cu, waves;
@@ -1461,10 +1508,12 @@ static const CfgInfo CFG[NCFG] = {
     {64, 256, 2, 4, 0.70f, true},   {128, 128, 2, 4, 0.67f, true},  {64, 128, 4, 2, 0.45f, true},
 };
 
-constexpr int NX = 4;
+constexpr int NX = 6;
 static const CfgInfo XCFG[NX] = {
     {64, 128, 2, 4, 0.40f, false}, {64, 64, 4, 2, 0.40f, false}, {64, 128, 4, 4, 0.40f, false}, {64, 64, 2, 2, 0.40f, false},
+    {64, 128, 2, 8, 0.40f, false}, {64, 128, 1, 8, 0.40f, false},
 };
+static const int XKSP_BK[NX] = {0, 0, 0, 0, 64, 128};  // K-group configurations: their stage size
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
 static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1 + pb_count() + NX; }
@@ -1473,11 +1522,15 @@ static int rbp_first() { return NCFG + q16_count() + rb_count(); }
 static int dtab_first() { return rbp_first() + rbp_count(); }
 static int dhead_id() { return dtab_first() + dtab_count(); }  // configuration 44: the classifier head
 static int pb_first() { return dhead_id() + 1; }                 // configurations 45-49: persistent band
-static int xr_first() { return pb_first() + pb_count(); }         // configurations 50-53: extra ring tiles
+static int xr_first() { return pb_first() + pb_count(); }         // configurations 50-55: extra ring tiles
 
 static bool cfg_ok(int k, const Params& p) {
   if (k >= ncfg_all()) return false;
-  if (k >= xr_first()) return epi_kind(p.e) != EK_GEN || XCFG[k - xr_first()].bm * XCFG[k - xr_first()].bn < 65536;
+  if (k >= xr_first()) {
+    const int x = k - xr_first();
+    if (XKSP_BK[x] && (p.d.kpad / XKSP_BK[x]) % 2) return false;  // two K groups: an even stage count
+    return epi_kind(p.e) != EK_GEN || XCFG[x].bm * XCFG[x].bn < 65536;
+  }
   if (k >= pb_first()) return pb_ok(k - pb_first(), p);
   if (k == dhead_id()) return dhead_ok(p);
   if (k >= dtab_first()) return dtab_ok(k - dtab_first(), p);
@@ -1539,7 +1592,9 @@ static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, 
       case 0: return launch_ek<X0>(x, w, p, s);
       case 1: return launch_ek<X1>(x, w, p, s);
       case 2: return launch_ek<X2>(x, w, p, s);
-      default: return launch_ek<X3>(x, w, p, s);
+      case 3: return launch_ek<X3>(x, w, p, s);
+      case 4: return launch_ek<X4>(x, w, p, s);
+      default: return launch_ek<X5>(x, w, p, s);
     }
   }
   if (k >= pb_first()) return pb_launch(k - pb_first(), x, w, p, s);

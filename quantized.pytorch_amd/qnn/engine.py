@@ -74,7 +74,7 @@ class Engine:
     nothing) avoids the copy.  graph=False runs the launches eagerly (debugging)."""
 
     def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None, fuse_stem_pool=True,
-                 max_links=None, tiles=None):
+                 max_links=None, tiles=None, branches=None):
         """tile=k forces tile configuration k on every contraction it is built for (the
         others keep the cost model's choice); tile=None autotunes (or the cost model
         when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile.
@@ -84,8 +84,17 @@ class Engine:
         output an fp32 map); None = QNN_ENGINE_MAX_LINKS or QNN_MAX_RES.
         tiles: an explicit configuration per contraction (e.g. another rank's autotuned
         `engine.tiles`, qnn.dist.build_engine); one not built for this plan falls back to
-        the cost model's choice."""
+        the cost model's choice.
+        branches: run each residual block's downsample contraction on a second stream, concurrent
+        with the block's main-path convs (forked after the block input is ready, joined before
+        the block's last conv, which reads its codes); None = QNN_ENGINE_BRANCHES (default 1).
+        The outputs are bitwise the same either way (no two concurrent launches write a common
+        buffer or read one the other writes)."""
         self.fuse_stem_pool = fuse_stem_pool
+        if branches is None:
+            branches = os.environ.get("QNN_ENGINE_BRANCHES", "1") == "1"
+        self.branches = bool(branches)
+        self.forks = {}  # op index of a side-stream launch -> op index that must wait for it
         if max_links is None:
             max_links = int(os.environ.get("QNN_ENGINE_MAX_LINKS", _lib.MAX_RES))
         if not 0 <= max_links <= _lib.MAX_RES:
@@ -104,6 +113,7 @@ class Engine:
         self.launch_names = []
         self.launch_meta = []
         self.convs = []  # (op index, ConvDesc, Epilogue) of every contraction
+        self._side = None
         self._bn_cache = {}  # RangeBN module -> BnParams: each module's range is read exactly once
         with torch.no_grad():
             if hasattr(model, "features") and hasattr(model, "fc"):
@@ -444,11 +454,13 @@ class Engine:
         # recomputes RangeBN from them; an identity shortcut extends the block input's chain
         # by this block's own RangeBN codes, so no fp32 map is written or read until a
         # chain would exceed QNN_MAX_RES links (then this block writes an fp32 checkpoint).
+        ds_op = None
         if blk.downsample is not None:
             ds_conv, ds_bn = blk.downsample[0], blk.downsample[1]
             code = self._btiled(Ho, Wo, cout)
             self._conv(ds_conv, self._codes_for(x, ds_conv), x.H, x.W, bn=ds_bn, relu=False, out_bncode=code,
                        bncode_tiled=True)
+            ds_op = len(self.ops) - 1
             chain = (None, [(code, ds_bn)], False)
         else:
             chain = x.res
@@ -482,6 +494,8 @@ class Engine:
                        outs=[self._codes_for(a1, blk.conv2)[1]])
             self._conv(blk.conv2, self._codes_for(a1, blk.conv2), Ho, Wo, bn=blk.bn2, chain=chain, relu=True,
                        outs=outs, out_f32=f32, out_bncode=bnc, bncode_tiled=True)
+        if ds_op is not None:  # the downsample's codes are read first by the block's last conv
+            self.forks[ds_op] = len(self.ops) - 1
         return out
 
     def _plan_head(self, model, x, pool_k):
@@ -657,8 +671,34 @@ class Engine:
 
     def _run_ops(self):
         st = _lib.stream_of(self.input)  # the current stream (the capture stream while capturing)
-        for op in self.ops:
-            op(st)
+        if not (self.branches and self.forks):
+            for op in self.ops:
+                op(st)
+            return
+        # fork / join on a second stream (recorded into the hipGraph as parallel branches when
+        # capturing): each side launch waits for everything issued before it on the main stream
+        main = torch.cuda.current_stream(self.dev)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        side = self._side
+        sst = ctypes.c_void_p(side.cuda_stream)
+        joins = {}
+        for i, op in enumerate(self.ops):
+            ev = joins.pop(i, None)
+            if ev is not None:
+                main.wait_event(ev)
+            if i in self.forks:
+                fork = torch.cuda.Event()
+                fork.record(main)
+                side.wait_event(fork)
+                op(sst)
+                done = torch.cuda.Event()
+                done.record(side)
+                joins[self.forks[i]] = done
+            else:
+                op(st)
+        for ev in joins.values():  # (none: every fork joins inside the forward)
+            main.wait_event(ev)
 
     def _capture(self):
         s = torch.cuda.Stream(device=self.dev)

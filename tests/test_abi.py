@@ -101,7 +101,7 @@ def test_tile_kernel_families(lib):
     # table-epilogue direct configurations (ids of earlier families never move)
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
     # the ring family is split by the ping-pong ids 6-9 and again by ids 12-49 (round 5 appended
-    # ring configurations 50-53), the direct family by ids 40-43 (the classifier head, 44, is a
+    # ring configurations 50-55), the direct family by ids 40-43 (the classifier head, 44, is a
     # direct-fragment configuration appended in round 4)
     assert len(runs) == len(set(runs)) + 3
     assert len(_lib.tile_ids("qconv_direct_kernel")) == 6 and _lib.tile_ids("qconv_direct_kernel")[-1] == 44
@@ -110,7 +110,7 @@ def test_tile_kernel_families(lib):
     assert fams[44] == "qconv_direct_kernel"
     # round 5 appended the persistent-band configurations 45-49
     assert _lib.tile_ids("qconv_pb_kernel") == [45, 46, 47, 48, 49]
-    assert [fams[k] for k in range(50, 54)] == ["qconv_kernel"] * 4 and len(fams) == 54
+    assert [fams[k] for k in range(50, 56)] == ["qconv_kernel"] * 6 and len(fams) == 56
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 

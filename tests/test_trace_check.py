@@ -58,7 +58,7 @@ def test_trace_check_accepts_consistent_trace(tmp_path):
     r = json.load(open(out))
     assert abs(r["trace_kernel_ms_per_forward"] - 0.175) < 1e-9
     assert abs(r["trace_conv_ms_per_forward"] - 0.150) < 1e-9
-    assert r["checks"] == {"trace_sum_le_ms_per_step": True, "frac_within_5pct": True}
+    assert r["checks"] == {"trace_busy_le_ms_per_step": True, "frac_within_5pct": True}
     assert [x["us"] for x in r["launches"]] == [20.0, 100.0, 50.0, 5.0]
 
 
@@ -80,3 +80,44 @@ def test_trace_check_anchors_on_the_input_quantizer(tmp_path):
     r = json.load(open(out))
     assert r["launches"][0]["kernel"].startswith("quantize_s2d")
     assert [x["us"] for x in r["launches"]] == [20.0, 100.0, 50.0, 5.0]
+
+
+def test_trace_check_concurrent_branches(tmp_path):
+    """Forwards whose two middle launches run concurrently, starting in either order: the blocks
+    are still found, each launch is matched by name, and the busy time counts overlap once."""
+    import trace_check
+    rows, t = [], 1_000_000
+    names = [NAMES[0], NAMES[1], "void qnn::qconv_kernel<ds>(int)", NAMES[2], NAMES[3]]
+    for f in range(26):
+        rows.append({"Kernel_Name": names[0], "Start_Timestamp": t, "End_Timestamp": t + 20_000})
+        t += 21_000
+        rows.append({"Kernel_Name": names[1], "Start_Timestamp": t, "End_Timestamp": t + 100_000})
+        t += 101_000
+        a, b = (names[2], names[3]) if f % 2 else (names[3], names[2])
+        da, db = (10_000, 50_000) if a == names[2] else (50_000, 10_000)
+        rows.append({"Kernel_Name": a, "Start_Timestamp": t, "End_Timestamp": t + da})
+        rows.append({"Kernel_Name": b, "Start_Timestamp": t + 500, "End_Timestamp": t + 500 + db})
+        t += 51_000
+        rows.append({"Kernel_Name": names[4], "Start_Timestamp": t, "End_Timestamp": t + 5_000})
+        t += 6_000
+    trace = str(tmp_path / "run_kernel_trace.csv")
+    with open(trace, "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        w.writerows(rows)
+    conv_busy_ms = 0.1505  # stem 100 us + the concurrent pair 50.5 us
+    ops = 1e12 * 0.75
+    line = {"steps": 20, "ms_per_step": 0.19, "engine": {"launches_per_forward": 5},
+            "roofline": {"achieved": ops / (conv_busy_ms * 1e-3) / 1e12,
+                         "frac": ops / (conv_busy_ms * 1e-3) / 1e12 / 5000.0, "kernel_ms_per_forward": conv_busy_ms}}
+    bj = str(tmp_path / "bench.json")
+    open(bj, "w").write(json.dumps(line) + "\n")
+    out = str(tmp_path / "out.json")
+    assert trace_check.main(trace, bj, out) == 0
+    r = json.load(open(out))
+    assert abs(r["trace_kernel_ms_per_forward"] - 0.185) < 1e-9
+    # the pair covers 50.5 us when the short launch starts first, 50 when the long one does
+    assert abs(r["trace_busy_ms_per_forward"] - 0.17525) < 1e-4
+    assert abs(r["trace_conv_ms_per_forward"] - 0.15025) < 1e-4
+    us = {x["kernel"]: x["us"] for x in r["launches"]}
+    assert us["qconv_kernel<ds>"] == 10.0 and us["qconv_kernel<qnn::Cfg<1>>"] == 50.0
