@@ -87,12 +87,15 @@ class Engine:
         the cost model's choice.
         branches: run each residual block's downsample contraction on a second stream, concurrent
         with the block's main-path convs (forked after the block input is ready, joined before
-        the block's last conv, which reads its codes); None = QNN_ENGINE_BRANCHES (default 1).
+        the block's last conv, which reads its codes); None = QNN_ENGINE_BRANCHES (default 0).
         The outputs are bitwise the same either way (no two concurrent launches write a common
-        buffer or read one the other writes)."""
+        buffer or read one the other writes).  Measured slower (ResNet-18 b128 160.1 K vs 164.2 K
+        img/s serial, ResNet-50 b256 56.8 K vs 57.2 K): the graph's fork/join edges widen the
+        gaps between launches (trace busy time 0.760 of 0.830 ms per forward, against 0.794 of
+        0.815 serial) by more than the overlap saves, so the serial order is the default."""
         self.fuse_stem_pool = fuse_stem_pool
         if branches is None:
-            branches = os.environ.get("QNN_ENGINE_BRANCHES", "1") == "1"
+            branches = os.environ.get("QNN_ENGINE_BRANCHES", "0") == "1"
         self.branches = bool(branches)
         self.forks = {}  # op index of a side-stream launch -> op index that must wait for it
         if max_links is None:

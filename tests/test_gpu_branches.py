@@ -18,7 +18,7 @@ def test_branches_bitwise_vs_serial(gpu, depth, batch):
     x = synthetic.input_batch((batch, 3, 224, 224), 77).to(gpu)
     ser = Engine(model, batch, autotune=False, branches=False)
     par = Engine(model, batch, autotune=False, branches=True)
-    assert par.forks and not ser.branches
+    assert par.forks and par.branches and not ser.branches
     assert len(par.forks) == (3 if depth == 18 else 4)
     with torch.no_grad():
         ref = ser(x).clone()
