@@ -52,7 +52,8 @@ namespace sp {
 constexpr int C = 64;    // stem channels (one 64-channel block, 4 MFMA row tiles)
 constexpr int TM = 4;
 #ifndef QNN_SP_W
-#define QNN_SP_W 8
+#define QNN_SP_W 12  // three waves per SIMD (measured: 8 waves 97.5 / 184.8 us, 12 waves 90.0 / 165-168 at
+                     // ResNet-18 b128 / ResNet-50 b256, profiles/r5_stem_ablation.txt)
 #endif
 #ifndef QNN_SP_DB
 #define QNN_SP_DB 1
@@ -62,6 +63,9 @@ constexpr int W = QNN_SP_W;  // waves: each takes every W-th 16-pixel stem tile,
 // under this item's pooling (less LDS: more blocks per CU)
 constexpr bool DB = QNN_SP_DB;
 constexpr int NT = 64 * W;
+// more than two waves per SIMD (QNN_SP_W 12: three): the VGPR budget drops to 168, so the
+// channel vectors are read from LDS where used and the tiles are not software-pipelined
+constexpr bool LEAN = W > 8;
 #ifndef QNN_SP_PR
 #define QNN_SP_PR 4
 #endif
@@ -105,7 +109,7 @@ struct Pool {
   const int8_t* lut1;
   qnn_code_out c1;
   int nitems;            // n * nrg
-  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc, lds_band, lds_band_bytes, lds_zero;  // LDS offsets
+  int lds_codes, lds_lut0, lds_lut1, lds_dir, lds_hc, lds_band, lds_band_bytes, lds_zero, lds_mask;  // LDS offsets
 };
 
 template <int KS, bool MASKED, bool BIAS>
@@ -169,6 +173,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   int* s_hc = reinterpret_cast<int*>(smem + pl.lds_hc);
   for (int i = tid; i < d.ho + d.wo; i += NT) s_hc[i] = i < d.ho ? e.hcls[i] * e.nwc : e.wcls[i - d.ho];
   if (tid < 4) reinterpret_cast<int*>(smem + pl.lds_zero)[tid] = 0;
+  if constexpr (MASKED && LEAN)  // the K mask, read per tile (no registers to hold it)
+    for (int i = tid; i < d.kpad / 16; i += NT)
+      *reinterpret_cast<v4i*>(smem + pl.lds_mask + 16 * i) = *reinterpret_cast<const v4i*>(d.kmask + 16 * i);
 
   // ---- the K chunks of this lane: tap u / cpg, 16 channels each, as band byte offsets from
   // the tile pixel's tap (0, 0); chunks past the taps read a 16-byte zero slot
@@ -183,7 +190,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
 #pragma unroll
     for (int i = 0; i < TM; ++i)
       fa[s][i] = *reinterpret_cast<const v4i*>(w + (int64_t)(16 * i + (lane & 15)) * d.kpad + 64 * s + 16 * g);
-    if constexpr (MASKED) ones[s] = *reinterpret_cast<const v4i*>(d.kmask + 64 * s + 16 * g);
+    if constexpr (MASKED && !LEAN) ones[s] = *reinterpret_cast<const v4i*>(d.kmask + 64 * s + 16 * g);
     else ones[s] = (v4i){0x01010101, 0x01010101, 0x01010101, 0x01010101};
   }
   wait_vmcnt<0>();  // staged data, tables, weights (and the first band)
@@ -191,12 +198,15 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
   const float* s_f = reinterpret_cast<const float*>(smem);
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
   float4 sw[TM], bw[TM], bi[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  auto chan_vecs = [&](int i) {  // the channel vectors of row tile i (LEAN: read at use)
     const int cl = 16 * i + 4 * g;
     sw[i] = *reinterpret_cast<const float4*>(s_f + cl);
     bw[i] = *reinterpret_cast<const float4*>(s_f + C + cl);
-    bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * C + cl);
+    if constexpr (BIAS) bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * C + cl);
+  };
+  if constexpr (!LEAN) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) chan_vecs(i);
   }
   // the stem codes, [stem pixel][64 bytes] with the channels of each pixel in LANE order: byte
   // 16 g + 4 i + u is channel 16 i + 4 g + u, so a tile lane (4 g) stores its 16 codes as one
@@ -280,7 +290,9 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
           A.s[0] += fb[s][0];
           continue;
         }
-        A.s = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones[s], fb[s], A.s, 0, 0, 0);
+        v4i o = ones[s];
+        if constexpr (MASKED && LEAN) o = *reinterpret_cast<const v4i*>(smem + pl.lds_mask + 64 * s + 16 * g);
+        A.s = __builtin_amdgcn_mfma_i32_16x16x64_i8(o, fb[s], A.s, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < TM; ++i) A.a[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[s][i], fb[s], A.a[i], 0, 0, 0);
       }
@@ -302,6 +314,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
       for (int i = 0; i < TM; ++i) {
         const int cl = 16 * i + 4 * g;
         const float4 tb = *reinterpret_cast<const float4*>(s_f + (7 + pc) * C + cl);
+        if constexpr (LEAN) chan_vecs(i);
         const v4i& a = A.a[i];
         const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
         // the exact decomposition with the op order of every conv epilogue (epi16.h conv_out4)
@@ -325,6 +338,16 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
         __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);  // VALU
       }
     };
+    if constexpr (LEAN) {
+      Acc A;
+      for (int t = wave; t < q.ntile; t += W) {
+        v4i fb[KS];
+        int lr, col;
+        load_b(t, fb, lr, col);
+        mfmas(fb, A);
+        epilogue(t, lr, col, A);
+      }
+    } else {
     Acc A0, A1;
     v4i fnx[KS];
     int t = wave, nlr = 0, ncol = 0, lrA = 0, colA = 0, lrB = 0, colB = 0;
@@ -350,6 +373,7 @@ __global__ __launch_bounds__(NT) void stem_pool_kernel(const int8_t* __restrict_
       epilogue(t, lrB, colB, A1);
       interleave();
       t += W;
+    }
     }
 #if QNN_STAMP
     SP_TS(tb);
@@ -465,6 +489,8 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, const Pool&
   off += pl.lut1 ? 256 * C : 0;
   pl.lds_zero = off;
   off += 16;
+  pl.lds_mask = off;  // (LEAN + masked: the K mask, kpad <= 256 bytes)
+  off += LEAN && p.d.kmask ? 256 : 0;
   pl.lds_band = off;  // two bands: (2 PR + 1) stem rows read (2 PR) * sh + kh padded input rows, 1 KiB pieces
   pl.lds_band_bytes = (int)cdiv((int64_t)(2 * PR * p.d.sh + p.d.kh) * p.d.wp * p.d.cp, 1024) * 1024;
   off += (DB ? 2 : 1) * pl.lds_band_bytes;
