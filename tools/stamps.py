@@ -33,7 +33,9 @@ def plan(d, e=None):
     e = e if e is not None else _lib.Epilogue(mode=1)
     _lib.call("qnn_conv_plan", ctypes.byref(d), ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(bm),
               ctypes.byref(bn), ctypes.byref(nblk))
-    waves = [8, 8, 8, 4, 4, 2, 8, 8, 8, 8, 4, 4, 8, 8, 8, 4, 4, 2][cfg.value]  # qconv.hip CFG[].waves
+    # qconv.hip CFG[].waves (0-17) and XCFG[].waves (50-55); other families are not stamped here
+    waves = {**dict(enumerate([8, 8, 8, 4, 4, 2, 8, 8, 8, 8, 4, 4, 8, 8, 8, 4, 4, 2])),
+             **dict(zip(range(50, 56), [4, 2, 4, 2, 8, 8]))}.get(cfg.value)
     return cfg.value, waves, nblk.value
 
 
@@ -130,6 +132,9 @@ def main():
                     continue
                 M = d.n * d.ho * d.wo
                 cfg_, W, nblk = plan(d, e)
+                if W is None:
+                    print(f"engine launch {i}: configuration {cfg_} is not a qconv.hip kernel (no stamps)")
+                    continue
                 report(f"engine launch {i} M={M} cout={d.cout} K={d.kh * d.kw * d.cp} cfg={cfg_}", read(nblk, W))
 
 
