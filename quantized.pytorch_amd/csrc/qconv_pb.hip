@@ -608,9 +608,20 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   constexpr int STORES = TM == 4 ? 1 : TM;
   const bool counted = EK == EK_LUT && g.lut && QNN_ABLATE != 2;
   bool tile_since_issue = false;
+  // EK_GEN: the vector-memory instructions a tile issues after its band DMA -- the residual
+  // chain's prefetch (gen_prefetch) and the epilogue's stores, only those every tile issues
+  // (at most the true count: vector memory completes in issue order, so waiting until no more
+  // than these are in flight still covers the older band pieces)
+  int gen_young = 0;
+  if constexpr (EK == EK_GEN) {
+    const qnn_epilogue& e = p.e;
+    gen_young = TM * (e.nres + (e.residual ? 1 : 0) + (e.bn_mean && e.out_bncode ? 1 : 0) + (e.out_f32 ? 1 : 0) +
+                      (e.out_code0 && e.code0_cp >= d.cout ? 1 : 0) + (e.out_code1 && e.code1_cp >= d.cout ? 1 : 0));
+  }
   auto publish = [&] {  // this wave's pieces of the bands it issued have landed
     if (published < issued) {
       if (counted && tile_since_issue) wait_vmcnt<STORES>();
+      else if (EK == EK_GEN && tile_since_issue) wait_vmcnt_rt(gen_young);
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         for (int j = published; j < issued; ++j) lds_add(&s_sync[j & 1], 1);
@@ -654,7 +665,10 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
       issue_band(issued++);
       tile_since_issue = false;
     }
-    publish();
+    // this wave's own pieces of band j must be published before it waits for the band; younger
+    // bands' pieces just issued stay in flight (published at the next tile start: no wave can be
+    // waiting for them before band j is complete, so holding them cannot deadlock)
+    if (published <= j) publish();
     {
       const int target = C::W * (j / 2 + 1);
       for (int guard = 0; lds_get(&s_sync[j & 1]) < target && guard < SPIN_MAX; ++guard) __builtin_amdgcn_s_sleep(1);
