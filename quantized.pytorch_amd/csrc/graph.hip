@@ -234,9 +234,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
                                                       int wo, float x_min, float x_scale, const float* bias,
                                                       qnn_bn_params bn, int has_bn, int relu,
                                                       float* out_f32, qnn_code_out c0, int rows, const int8_t* __restrict__ lut,
-                                                      int cs) {
+                                                      int cs, int xbytes) {
   constexpr int K = 3, NCOL = (R - 1) * S + K, CPT = 2 * P;  // CPT channels per thread
-  using LT = std::conditional_t<P == 4, uint2, uint32_t>;    // one tap of them: 8 or 4 code bytes
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  using LT = std::conditional_t<P == 4, u32x2, uint32_t>;    // one tap of them: 8 or 4 code bytes
   const int nsl = c / cs, ct = cs / CPT, per_blk = 256 / ct;
   const int tc = threadIdx.x % ct, tp = threadIdx.x / ct;
   const int nxg = (wo + R - 1) / R, total = rows * nxg;
@@ -287,8 +288,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   const QParams c0p = make_qparams(c0.neg_min, c0.scale, c0.qmax);
   const f2 xs2 = {x_scale, x_scale}, xm2 = {x_min, x_min};
   const f2 bs2 = {bn.scale, bn.scale}, bm2 = {bn.min, bn.min};
-  // (row, pixel group) of group g: float reciprocals with an exact fix-up (groups < 2^24 on
-  // the host), integer division otherwise
+  // (image, output row, pixel group) of group g: float reciprocals with an exact fix-up (groups
+  // < 2^24 on the host), integer division otherwise -- once per thread; every later group is the
+  // previous one advanced by the grid stride, in the same three coordinates
   const bool fdiv = total < (1 << 24);
   const float inv_nxg = 1.0f / (float)nxg, inv_ho = 1.0f / (float)ho;
   auto divmod = [&](int m, int D, float invD, int& q, int& r) __attribute__((always_inline)) {
@@ -301,36 +303,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
       q = m / D, r = m - q * D;
     }
   };
-  // Every load unconditional (clamped in-buffer addresses: the padded buffer holds any row
-  // oy*S + r and column < wp) and all K x NCOL issued together -- a load under a branch
-  // gets its own vmcnt(0) wait.  Software-pipelined: the next group's loads are in flight
-  // while this group computes.
-  // in-image offsets in 32 bits (a padded image is < 2^31 bytes on the host), one 64-bit base
+  struct Pos {
+    int img, oy, xg;
+  };
+  const int step = (gridDim.x / nsl) * per_blk;  // grid stride in groups (wave-uniform)
+  const int st_row = step / nxg, st_xg = step - st_row * nxg, st_img = st_row / ho, st_oy = st_row - st_img * ho;
+  auto advance = [&](Pos& q) __attribute__((always_inline)) {
+    int dr = st_oy;
+    q.xg += st_xg;
+    if (q.xg >= nxg) q.xg -= nxg, ++dr;
+    q.oy += dr;
+    q.img += st_img;
+    if (q.oy >= ho) q.oy -= ho, ++q.img;
+  };
+  // The input as a buffer resource over its n*hp*wp*cp bytes (< 2^31 on the host): a tap load is
+  // one 32-bit offset add, and a load past the end (the prefetch of the group after a thread's
+  // last) returns zeros instead of faulting -- no clamping.  Every load is unconditional and all
+  // K x NCOL are issued together (a load under a branch gets its own vmcnt(0) wait); the next
+  // group's loads are in flight while this group computes.  Columns past a row's end read the
+  // next row's bytes (or zeros): only taps outside the image read them, and those are skipped.
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, xbytes, 0x00020000);
   const int wpcp = wp * cp;
-  auto load = [&](int g, LT (&v)[K][NCOL]) __attribute__((always_inline)) {
-    int row, xg, img, oy;
-    divmod(g, nxg, inv_nxg, row, xg);
-    divmod(row, ho, inv_ho, img, oy);
-    const int8_t* xrow = x + (size_t)(img * hp + oy * S) * (size_t)wpcp + cb;
+  auto load = [&](const Pos& q, LT (&v)[K][NCOL]) __attribute__((always_inline)) {
+    const uint32_t base = ((uint32_t)(q.img * hp + q.oy * S) * (uint32_t)wp + (uint32_t)(q.xg * R * S)) * (uint32_t)cp +
+                          (uint32_t)cb;
 #pragma unroll
     for (int r = 0; r < K; ++r)
 #pragma unroll
       for (int col = 0; col < NCOL; ++col) {
-        const int px = min(xg * R * S + col, wp - 1);
-        v[r][col] = *reinterpret_cast<const LT*>(xrow + (r * wpcp + (int)__umul24((unsigned)px, (unsigned)cp)));
+        const uint32_t o = base + (uint32_t)(r * wpcp + col * cp);
+        if constexpr (P == 4) v[r][col] = __builtin_amdgcn_raw_buffer_load_b64(xrs, o, 0, 0);
+        else v[r][col] = __builtin_amdgcn_raw_buffer_load_b32(xrs, o, 0, 0);
       }
   };
-  // grid-stride over (row, R-pixel group): the register-resident parameters are loaded
-  // once per thread and reused across all of its groups
-  const int step = (gridDim.x / nsl) * per_blk;
   // one pixel group on operands v, the next group's loads into vn (two groups per trip, the
   // buffers alternating: no register copies)
-  auto group = [&](int pg, LT (&v)[K][NCOL], LT (&vn)[K][NCOL]) __attribute__((always_inline)) {
-    int row, xg, img, oy;
-    divmod(pg, nxg, inv_nxg, row, xg);
-    divmod(row, ho, inv_ho, img, oy);
-    const int ox0 = xg * R;
-    load(min(pg + step, total - 1), vn);
+  auto group = [&](const Pos& cur, const Pos& nxt, LT (&v)[K][NCOL], LT (&vn)[K][NCOL]) __attribute__((always_inline)) {
+    const int img = cur.img, oy = cur.oy;
+    const int ox0 = cur.xg * R;
+    load(nxt, vn);
     f2 acc[R][P];
 #pragma unroll
     for (int j = 0; j < R; ++j)
@@ -426,12 +437,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
     }
   };
   LT va[K][NCOL], vb[K][NCOL];
-  load(pblk * per_blk + tp, va);
+  Pos cur, nxt;
+  {
+    int row;
+    divmod(pblk * per_blk + tp, nxg, inv_nxg, row, cur.xg);
+    divmod(row, ho, inv_ho, cur.img, cur.oy);
+  }
+  nxt = cur;
+  advance(nxt);
+  load(cur, va);
   for (int pg = pblk * per_blk + tp; pg < total;) {
-    group(pg, va, vb);
+    group(cur, nxt, va, vb);
+    cur = nxt;
+    advance(nxt);
     pg += step;
     if (pg >= total) break;
-    group(pg, vb, va);
+    group(cur, nxt, vb, va);
+    cur = nxt;
+    advance(nxt);
     pg += step;
   }
 }
@@ -570,7 +593,7 @@ static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, i
                     (!out_f32 || (((uintptr_t)out_f32) & 15) == 0) &&
                     (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0 &&
                                  (int64_t)n * c0.hp * c0.wp < (1LL << 31))) &&  // 32-bit pixel indices
-                    (int64_t)n * hp < (1LL << 31) && 3LL * wp * cp < (1LL << 31);
+                    (int64_t)n * hp * wp * cp < (1LL << 31);  // 32-bit buffer offsets
   // the table path: codes only, channel slices of 128 (or all c) channels
   const int cs = lut ? (c > 128 ? 128 : c) : c;
   const bool fast_lut = fast && lut && !out_f32 && c % cs == 0 && (((uintptr_t)lut) & 15) == 0;
@@ -592,7 +615,8 @@ static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, i
     const int64_t pblocks = std::min<int64_t>(cdiv(groups, 256 / ct), std::max<int64_t>(1, (int64_t)num_cu * per_cu / nsl));
     const int blocks = (int)(pblocks * nsl);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, (hipStream_t)stream, x, h, w, pad, hp, wp, cp, c, w_hat_t,
-                       ho, wo, x_min, x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0, rows, lut, cs);
+                       ho, wo, x_min, x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0, rows, lut, cs,
+                       (int)((int64_t)n * hp * wp * cp));
     QNN_LAUNCH_CHECK("qnn_dwconv_fused");
     return QNN_OK;
   }
