@@ -9,11 +9,17 @@
 
 #include "qconv_common.h"
 
+// depthwise 3x3 thread shape (MobileNet b512 depthwise, in-graph: 8 channels x 1 x 4 pixels at two
+// waves per SIMD 1.08-1.09 ms; 4 channels x 2 x 4 at three 1.006-1.009, x 3 x 4 / x 4 x 4 at two
+// 0.997-1.023 -- profiles/r5_dw_occupancy_ab.txt)
 #ifndef QNN_DW_WPE
-#define QNN_DW_WPE 2  // depthwise: waves per SIMD the register budget is sized for
+#define QNN_DW_WPE 3  // depthwise: waves per SIMD the register budget is sized for
 #endif
 #ifndef QNN_DW_P
-#define QNN_DW_P 4  // depthwise: channel pairs per thread (4: 8 channels, 8-byte loads; 2: 4 channels)
+#define QNN_DW_P 2  // depthwise: channel pairs per thread (4: 8 channels, 8-byte loads; 2: 4 channels)
+#endif
+#ifndef QNN_DW_RR
+#define QNN_DW_RR 2  // depthwise: output rows per thread
 #endif
 
 namespace qnn {
@@ -216,26 +222,28 @@ __global__ void dwconv_fused_kernel(const int8_t* __restrict__ x, int n, int h, 
 // dwconv_fused_kernel (so bitwise equal to it and to the module path): each tap's
 // x_hat = fl(fl(q*s)+min), fmaf into the accumulator in (r, s) row-major order with
 // out-of-image taps skipped, + bias, RangeBN on its quantized input, ReLU, the
-// consumer's codes.  Layout of the work instead: a thread owns 8 channels (8-byte
-// loads, coalesced along channels across the ct = cs/8 channel threads) of R
-// consecutive output pixels of one row, so each input column is dequantized once
-// and feeds up to 3 outputs from registers; the 9x8 tap weights, the bias and the
-// RangeBN vectors live in registers; both quantizers run division-free
-// (quant_code_fast, bit-identical); no 64-bit index arithmetic.
+// consumer's codes.  Layout of the work instead: a thread owns CPT channels (4: 4-byte
+// loads, coalesced along channels across the ct = cs/CPT channel threads) of an RR x R
+// block of output pixels (2 rows x 4 or 2 columns), so each input pixel of the block's
+// windows is dequantized once and feeds up to 9 outputs from registers; the 9 x CPT tap
+// weights, the bias and the RangeBN vectors live in registers; both quantizers run
+// division-free (quant_code_fast, bit-identical); 32-bit buffer offsets.
 // LUT (qnn_dwconv_fused_lut): RangeBN -> ReLU -> the consumer's quantizer of each channel is
 // the exact per-channel table qnn_bn_code_lut builds over the RangeBN input code (the conv
 // kernels' EK_LUT), so after the RangeBN input quotient each code is one LDS byte lookup --
 // half the kernel's VALU work per output was that chain.  A block then covers a slice of cs
 // channels (<= 128: a 32 KiB table slice in LDS), blocks of one pixel range and every slice
 // adjacent in the XCD-grouped order.
-template <int S, int R, int P, bool LUT>
+template <int S, int R, int P, bool LUT, int RR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE))) void dwconv3_kernel(const int8_t* __restrict__ x, int h, int w, int pad, int hp,
                                                       int wp, int cp, int c, const float* __restrict__ wt, int ho,
                                                       int wo, float x_min, float x_scale, const float* bias,
                                                       qnn_bn_params bn, int has_bn, int relu,
                                                       float* out_f32, qnn_code_out c0, int rows, const int8_t* __restrict__ lut,
                                                       int cs, int xbytes) {
-  constexpr int K = 3, NCOL = (R - 1) * S + K, CPT = 2 * P;  // CPT channels per thread
+  // a thread: CPT channels of an RR x R block of output pixels (RR rows, R columns), reading
+  // the KR x NCOL input pixels of their windows once
+  constexpr int K = 3, NCOL = (R - 1) * S + K, KR = (RR - 1) * S + K, CPT = 2 * P;
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   using LT = std::conditional_t<P == 4, u32x2, uint32_t>;    // one tap of them: 8 or 4 code bytes
   const int nsl = c / cs, ct = cs / CPT, per_blk = 256 / ct;
@@ -291,7 +299,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   // < 2^24 on the host), integer division otherwise -- once per thread; every later group is the
   // previous one advanced by the grid stride, in the same three coordinates
   const bool fdiv = total < (1 << 24);
-  const float inv_nxg = 1.0f / (float)nxg, inv_ho = 1.0f / (float)ho;
+  const int nyg = (ho + RR - 1) / RR;  // row groups per image (rows = n * nyg)
+  const float inv_nxg = 1.0f / (float)nxg, inv_nyg = 1.0f / (float)nyg;
   auto divmod = [&](int m, int D, float invD, int& q, int& r) __attribute__((always_inline)) {
     if (fdiv) {
       q = (int)((float)m * invD);
@@ -303,17 +312,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
     }
   };
   struct Pos {
-    int img, oy, xg;
+    int img, oy, xg;  // oy: the group's first output row (a multiple of RR)
   };
   const int step = (gridDim.x / nsl) * per_blk;  // grid stride in groups (wave-uniform)
-  const int st_row = step / nxg, st_xg = step - st_row * nxg, st_img = st_row / ho, st_oy = st_row - st_img * ho;
+  const int st_row = step / nxg, st_xg = step - st_row * nxg, st_img = st_row / nyg;
+  const int st_oy = (st_row - st_img * nyg) * RR, hoR = nyg * RR;
   auto advance = [&](Pos& q) __attribute__((always_inline)) {
     int dr = st_oy;
     q.xg += st_xg;
-    if (q.xg >= nxg) q.xg -= nxg, ++dr;
+    if (q.xg >= nxg) q.xg -= nxg, dr += RR;
     q.oy += dr;
     q.img += st_img;
-    if (q.oy >= ho) q.oy -= ho, ++q.img;
+    if (q.oy >= hoR) q.oy -= hoR, ++q.img;
   };
   // The input as a buffer resource over its n*hp*wp*cp bytes (< 2^31 on the host): a tap load is
   // one 32-bit offset add, and a load past the end (the prefetch of the group after a thread's
@@ -323,11 +333,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   // next row's bytes (or zeros): only taps outside the image read them, and those are skipped.
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, xbytes, 0x00020000);
   const int wpcp = wp * cp;
-  auto load = [&](const Pos& q, LT (&v)[K][NCOL]) __attribute__((always_inline)) {
+  auto load = [&](const Pos& q, LT (&v)[KR][NCOL]) __attribute__((always_inline)) {
     const uint32_t base = ((uint32_t)(q.img * hp + q.oy * S) * (uint32_t)wp + (uint32_t)(q.xg * R * S)) * (uint32_t)cp +
                           (uint32_t)cb;
 #pragma unroll
-    for (int r = 0; r < K; ++r)
+    for (int r = 0; r < KR; ++r)
 #pragma unroll
       for (int col = 0; col < NCOL; ++col) {
         const uint32_t o = base + (uint32_t)(r * wpcp + col * cp);
@@ -337,24 +347,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   };
   // one pixel group on operands v, the next group's loads into vn (two groups per trip, the
   // buffers alternating: no register copies)
-  auto group = [&](const Pos& cur, const Pos& nxt, LT (&v)[K][NCOL], LT (&vn)[K][NCOL]) __attribute__((always_inline)) {
-    const int img = cur.img, oy = cur.oy;
+  auto group = [&](const Pos& cur, const Pos& nxt, LT (&v)[KR][NCOL], LT (&vn)[KR][NCOL]) __attribute__((always_inline)) {
+    const int img = cur.img, oy0 = cur.oy;
     const int ox0 = cur.xg * R;
     load(nxt, vn);
-    f2 acc[R][P];
+    f2 acc[RR][R][P];
 #pragma unroll
-    for (int j = 0; j < R; ++j)
+    for (int i = 0; i < RR; ++i)
 #pragma unroll
-      for (int p = 0; p < P; ++p) acc[j][p] = (f2){0.f, 0.f};
+      for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int p = 0; p < P; ++p) acc[i][j][p] = (f2){0.f, 0.f};
 
     // Taps outside the image (zero padding of x_hat), LUT kernels: without branches -- their
     // x_hat is made +0 exactly (q * 0 + 0), and fma(+0, w, acc) = acc for every acc the chain can
     // hold (it starts at +0 and an exact zero sum rounds to +0, so it is never -0): bitwise the
     // skipped tap, measured -4 % on MobileNet's depthwise layers.  The fp32-output kernels keep
     // the branches (the selects' registers would spill there).
+    // (input row ri feeds output row i through kernel row ri - i S: each output's taps are
+    // accumulated in row-major (r, s) order, as the generic kernel does)
 #pragma unroll
-    for (int r = 0; r < K; ++r) {
-      const bool rok = (unsigned)(oy * S + r - pad) < (unsigned)h;
+    for (int r = 0; r < KR; ++r) {
+      const bool rok = (unsigned)(oy0 * S + r - pad) < (unsigned)h;
 #pragma unroll
       for (int col = 0; col < NCOL; ++col) {
         const bool ok = rok && (unsigned)(ox0 * S + col - pad) < (unsigned)w;
@@ -375,19 +389,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
         }
         (void)hi;
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-          const int s = col - j * S;
-          if (s < 0 || s >= K) continue;  // compile-time
+        for (int i = 0; i < RR; ++i) {
+          const int kr = r - i * S;
+          if (kr < 0 || kr >= K) continue;  // compile-time
 #pragma unroll
-          for (int p = 0; p < P; ++p) acc[j][p] = pfma(xh[p], wv[r * K + s][p], acc[j][p]);
+          for (int j = 0; j < R; ++j) {
+            const int s = col - j * S;
+            if (s < 0 || s >= K) continue;  // compile-time
+#pragma unroll
+            for (int p = 0; p < P; ++p) acc[i][j][p] = pfma(xh[p], wv[kr * K + s][p], acc[i][j][p]);
+          }
         }
       }
     }
 
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int ox = ox0 + j;
-      if (ox >= wo) break;
+    for (int ij = 0; ij < RR * R; ++ij) {
+      const int i = ij / R, j = ij % R;
+      const int oy = oy0 + i, ox = ox0 + j;
+      if (ox >= wo || oy >= ho) continue;
       if constexpr (LUT) {
         // RangeBN's input code per channel (the low mantissa byte of the magic-shifted clamped
         // quotient = its rint), then the consumer's code from the slice's table
@@ -397,7 +417,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
           uint32_t wd = 0;
 #pragma unroll
           for (int p = p2; p < p2 + 2 && p < P; ++p) {
-            const f2 y = bias ? acc[j][p] + bi[p] : acc[j][p];
+            const f2 y = bias ? acc[i][j][p] + bi[p] : acc[i][j][p];
             const f2 m = qclamp2(y, bnp) + MAGIC_U8;
             const int ch = cbl + 2 * p;
             const uint32_t b0 = (uint8_t)s_lut[ch * 256 + (__float_as_uint(m.x) & 255u)];
@@ -414,7 +434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
       f2 val[P];
 #pragma unroll
       for (int p = 0; p < P; ++p) {
-        f2 y = bias ? acc[j][p] + bi[p] : acc[j][p];
+        f2 y = bias ? acc[i][j][p] + bi[p] : acc[i][j][p];
         if (has_bn) {  // bn_apply(quant_code(y)), quantize.py:488-499
           f2 o = rint2(qclamp2(y, bnp)) * bs2;
           o = o + bm2;
@@ -443,12 +463,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
       }
     }
   };
-  LT va[K][NCOL], vb[K][NCOL];
+  LT va[KR][NCOL], vb[KR][NCOL];
   Pos cur, nxt;
   {
     int row;
     divmod(pblk * per_blk + tp, nxg, inv_nxg, row, cur.xg);
-    divmod(row, ho, inv_ho, cur.img, cur.oy);
+    divmod(row, nyg, inv_nyg, cur.img, cur.oy);
+    cur.oy *= RR;
   }
   nxt = cur;
   advance(nxt);
@@ -608,11 +629,12 @@ static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, i
                                         "(and c % 128 == 0 above 128 channels), 16-byte aligned table");
   if (fast) {
     const int R = sh == 1 ? 4 : 2;  // stride 2: 2 pixels (5 input columns) per thread, register budget
-    const int rows = n * ho, ct = cs / CPT, nsl = c / cs;
+    constexpr int RR = QNN_DW_RR;
+    const int rows = n * ((ho + RR - 1) / RR), ct = cs / CPT, nsl = c / cs;  // row groups
     const int64_t groups = (int64_t)rows * ((wo + R - 1) / R);
     QNN_REQUIRE(groups < (1LL << 31) && (int64_t)n * hp * wp * cp < (1LL << 40), "depthwise too large");
-    auto kern = fast_lut ? (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, true> : dwconv3_kernel<2, 2, QNN_DW_P, true>)
-                         : (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, false> : dwconv3_kernel<2, 2, QNN_DW_P, false>);
+    auto kern = fast_lut ? (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, true, RR> : dwconv3_kernel<2, 2, QNN_DW_P, true, RR>)
+                         : (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, false, RR> : dwconv3_kernel<2, 2, QNN_DW_P, false, RR>);
     const int lds = fast_lut ? cs * 256 : 0;
     // grid-stride, sized to the resident capacity (the loop is software-pipelined); a whole
     // number of channel slices per pixel block

@@ -1,8 +1,9 @@
 """Fused depthwise kernel (MobileNet's depthwise QConv2d + RangeBN + ReLU + the pointwise
 consumer's quantizer, include/qnn.h qnn_dwconv_fused).
 
-The 3x3 fast kernel (dwconv3_kernel: 8 channels x 4 pixels per thread, register
-weights, division-free quantizers) restates the generic kernel's arithmetic op for
+The 3x3 fast kernel (dwconv3_kernel: 4 channels x a 2 x 4 (stride 2: 2 x 2) pixel block per
+thread, register weights, division-free quantizers, out-of-image taps masked to an exact
++0 in the code-table kernels) restates the generic kernel's arithmetic op for
 op, so both must agree BITWISE on every output (fp32 and codes) — over strides 1/2,
 larger maps and
 ragged widths (wo not a multiple of 4), channel counts whose c/8 does not divide 256,
@@ -39,6 +40,8 @@ def _run(xcodes, geom, wt, bias, bn, relu, out_f32, code, generic, st):
     (2, 56, 128, 1, True, True),
     (1, 112, 32, 1, True, True),
     (2, 29, 64, 2, True, True),    # odd extent, stride 2
+    (3, 17, 36, 1, True, True),    # odd output height (a row pair's second row past the map), c/4 = 9
+    (2, 10, 20, 2, False, True),   # stride 2, ho = 5: the last row pair half outside
     (1, 15, 96, 1, False, True),
 ])
 def test_dwconv_fast_equals_generic_bitwise(gpu, n, h, c, s, with_bias, with_bn):
