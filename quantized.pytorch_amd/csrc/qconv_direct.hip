@@ -56,8 +56,15 @@ __device__ __forceinline__ void fdivmod(int m, int D, float invD, int& q, int& r
   if (r >= D) ++q, r -= D;
 }
 
+// the register budget: two waves per SIMD (256 VGPRs).  With one (the budget of the prefetching
+// configurations until round 5) the 1x1 code-table launches took 180 VGPRs + 32 AGPRs -- two
+// waves resident anyway -- where two fit them in 147, three resident: MobileNet b512 in-graph
+// contractions 1.474-1.476 -> 1.41-1.44 ms, ResNet-18 b128 unchanged (gpurun_out/dkw A/B).
+#ifndef QNN_DK_WPE
+#define QNN_DK_WPE 2
+#endif
 template <class C, int EK, bool MASKED, int KS>
-__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu((C::PF || C::TN > 1) ? 1 : 2))) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(QNN_DK_WPE))) void qconv_direct_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ w,
                                                             const Params p) {
   constexpr int TM = C::TM, TN = C::TN, CB = C::CB, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
