@@ -72,10 +72,25 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(QNN_DK_WP
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  // persistent: block b owns channel tile b % nby and pixel tiles b / nby + k * (grid / nby)
+  // persistent: block b owns one channel tile and pixel tiles pt0 + k * (grid / nby).  With the
+  // grid a multiple of 8 * nby, block b sits on XCD b % 8 and the nby blocks of each pixel tile
+  // stream (b = 8 (q nby + cty) + x) share one XCD, so a pixel tile's input codes are fetched into
+  // one L2 once for all its channel tiles (qconv_dtab_kernel's mapping); else b % nby, b / nby
   const int nby = (d.cout + CB - 1) / CB;
-  const int c0 = (blockIdx.x % nby) * CB;
   const int pstep = gridDim.x / nby, npt = (p.M + BN - 1) / BN;
+  int cty, pt0;
+  {
+    const int G = gridDim.x, b = blockIdx.x;
+    if (G % (8 * nby) == 0) {
+      const int r = b >> 3;
+      cty = r % nby;
+      pt0 = (r / nby) * 8 + (b & 7);
+    } else {
+      cty = b % nby;
+      pt0 = b / nby;
+    }
+  }
+  const int c0 = cty * CB;
 
   // the epilogue's data by LDS-DMA, once per block
   stage_epi<C, EK>(p, x, smem, c0, wave, lane);
@@ -132,7 +147,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(QNN_DK_WP
   };
   v4i fnx[KS][TN];
   int nn[TN], nho[TN], nwo[TN];
-  int pt = blockIdx.x / nby;
+  int pt = pt0;
   if constexpr (C::PF) load_b(pt, fnx, nn, nho, nwo);
   // border classes in LDS past the epilogue data: hcls[ho] * nwc, then wcls[wo]
   int* s_hc = reinterpret_cast<int*>(smem + p.scr_off);
