@@ -406,7 +406,7 @@ int qnn_dwconv_fused_generic(const int8_t* x, int n, int h, int w, int pad, int 
 
 /* qnn_dwconv_fused with RangeBN -> ReLU -> the consumer's quantizer looked up instead of
  * evaluated: lut = qnn_bn_code_lut(bn, c, relu, code0) ([c][256] over the RangeBN input code,
- * bitwise the evaluated chain), codes out only, 3x3 stride 1 or 2, c % 8 == 0 (and c % 128 == 0
+ * bitwise the evaluated chain), codes out only, 3x3 stride 1 or 2, c % 4 == 0 (and c % 128 == 0
  * above 128 channels), lut 16-byte aligned; anything else is an argument error (round 4: the
  * MobileNet engine's depthwise launches). */
 int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, int wp, int cp, int c,

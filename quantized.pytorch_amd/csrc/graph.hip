@@ -620,19 +620,23 @@ static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, i
                     c / CPT <= 256 && cp % 8 == 0 && (((uintptr_t)x) & 7) == 0 && (((uintptr_t)w_hat_t) & 15) == 0 &&
                     (!out_f32 || (((uintptr_t)out_f32) & 15) == 0) &&
                     (!c0.ptr || (c0.cp % 8 == 0 && (((uintptr_t)c0.ptr) & 7) == 0 &&
-                                 (int64_t)n * c0.hp * c0.wp < (1LL << 31))) &&  // 32-bit pixel indices
-                    (int64_t)n * hp * wp * cp < (1LL << 31);  // 32-bit buffer offsets
+                                 (int64_t)c0.hp * c0.wp < (1LL << 31))) &&  // 32-bit pixel indices
+                    (int64_t)hp * wp * cp < (1LL << 31);  // 32-bit buffer offsets within an image
   // the table path: codes only, channel slices of 128 (or all c) channels
   const int cs = lut ? (c > 128 ? 128 : c) : c;
   const bool fast_lut = fast && lut && !out_f32 && c % cs == 0 && (((uintptr_t)lut) & 15) == 0;
-  if (lut && !fast_lut) return arg_error("qnn_dwconv_fused_lut: a 3x3 stride-1/2 layer with codes out only, c % 8 == 0 "
+  if (lut && !fast_lut) return arg_error("qnn_dwconv_fused_lut: a 3x3 stride-1/2 layer with codes out only, c % 4 == 0 "
                                         "(and c % 128 == 0 above 128 channels), 16-byte aligned table");
   if (fast) {
     const int R = sh == 1 ? 4 : 2;  // stride 2: 2 pixels (5 input columns) per thread, register budget
     constexpr int RR = QNN_DW_RR;
-    const int rows = n * ((ho + RR - 1) / RR), ct = cs / CPT, nsl = c / cs;  // row groups
-    const int64_t groups = (int64_t)rows * ((wo + R - 1) / R);
-    QNN_REQUIRE(groups < (1LL << 31) && (int64_t)n * hp * wp * cp < (1LL << 40), "depthwise too large");
+    // the kernel addresses its input by 32-bit offsets from one buffer resource and its code
+    // pixels by 32-bit indices: launched over chunks of images that keep both below 2^31
+    const int64_t img_in = (int64_t)hp * wp * cp, img_px = c0.ptr ? (int64_t)c0.hp * c0.wp : 1;
+    const int64_t lim = ((1LL << 31) - 1) / std::max(img_in, img_px);
+    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(n, lim));
+    const int ct = cs / CPT, nsl = c / cs;
+    QNN_REQUIRE((int64_t)nch * ((ho + RR - 1) / RR) * ((wo + R - 1) / R) < (1LL << 31), "depthwise too large");
     auto kern = fast_lut ? (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, true, RR> : dwconv3_kernel<2, 2, QNN_DW_P, true, RR>)
                          : (sh == 1 ? dwconv3_kernel<1, 4, QNN_DW_P, false, RR> : dwconv3_kernel<2, 2, QNN_DW_P, false, RR>);
     const int lds = fast_lut ? cs * 256 : 0;
@@ -641,12 +645,20 @@ static int dwconv_fused(const int8_t* x, int n, int h, int w, int pad, int hp, i
     const int num_cu = device_cu_count();
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    const int64_t pblocks = std::min<int64_t>(cdiv(groups, 256 / ct), std::max<int64_t>(1, (int64_t)num_cu * per_cu / nsl));
-    const int blocks = (int)(pblocks * nsl);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, (hipStream_t)stream, x, h, w, pad, hp, wp, cp, c, w_hat_t,
-                       ho, wo, x_min, x_scale, bias, b, bn ? 1 : 0, relu, out_f32, c0, rows, lut, cs,
-                       (int)((int64_t)n * hp * wp * cp));
-    QNN_LAUNCH_CHECK("qnn_dwconv_fused");
+    for (int i0 = 0; i0 < n; i0 += nch) {
+      const int ni = std::min(nch, n - i0);
+      const int rows = ni * ((ho + RR - 1) / RR);  // row groups
+      const int64_t groups = (int64_t)rows * ((wo + R - 1) / R);
+      const int64_t pblocks =
+          std::min<int64_t>(cdiv(groups, 256 / ct), std::max<int64_t>(1, (int64_t)num_cu * per_cu / nsl));
+      const int blocks = (int)(pblocks * nsl);
+      qnn_code_out ci = c0;
+      if (ci.ptr) ci.ptr += (int64_t)i0 * ci.hp * ci.wp * ci.cp;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, (hipStream_t)stream, x + i0 * img_in, h, w, pad, hp, wp,
+                         cp, c, w_hat_t, ho, wo, x_min, x_scale, bias, b, bn ? 1 : 0, relu,
+                         out_f32 ? out_f32 + (int64_t)i0 * ho * wo * c : nullptr, ci, rows, lut, cs, (int)(ni * img_in));
+      QNN_LAUNCH_CHECK("qnn_dwconv_fused");
+    }
     return QNN_OK;
   }
   hipLaunchKernelGGL(dwconv_fused_kernel, dim3(grid_for((int64_t)n * ho * wo * (c / 4))), dim3(256), 0,

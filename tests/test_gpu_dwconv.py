@@ -154,3 +154,40 @@ def test_dwconv_lut_refuses_unsupported(gpu):
     with pytest.raises(_lib.QnnError, match="qnn_dwconv_fused_lut"):
         _lib.call("qnn_dwconv_fused_lut", _lib.ptr(x), n, h, h, 1, h + 2, h + 2, c, c, _lib.ptr(wt), 3, 3, 1, 1, h, h,
                   -0.75, 0.01, None, ctypes.byref(bn), _lib.ptr(lut), ctypes.byref(code), _lib.stream_of(x))
+
+
+def test_dwconv_lut_chunked_past_2gib(gpu):
+    """Inputs past 2 GiB: the 3x3 kernel addresses an input by 32-bit buffer offsets, so the host
+    launches it over chunks of images (here 4 + 1 images of 514 MB); the codes match the generic
+    kernel's evaluated chain bitwise, the consumer's padding untouched."""
+    n, h, c, s = 5, 1000, 512, 1
+    k, pad = 3, 1
+    w, ho, wo, cp = h, h, h, c
+    hp, wp = h + 2 * pad, w + 2 * pad
+    assert n * hp * wp * cp >= 1 << 31
+    g = torch.Generator(device=gpu).manual_seed(77)
+    xg = torch.zeros((n, hp, wp, cp), dtype=torch.int8, device=gpu)
+    xg[:, pad:pad + h, pad:pad + w, :] = torch.randint(-128, 128, (n, h, w, c), generator=g, dtype=torch.int8,
+                                                        device=gpu)
+    xmin, xs = -0.75, 3.1 / 255
+    wt = torch.randn((k * k, c), generator=g, device=gpu) * 0.3
+    vecs = [torch.randn(c, generator=g, device=gpu) * 0.05, torch.rand(c, generator=g, device=gpu) + 0.5,
+            torch.rand(c, generator=g, device=gpu) * 2 - 0.5, torch.randn(c, generator=g, device=gpu) * 0.1]
+    bn = _lib.BnParams(*[_lib.ptr(v) for v in vecs], 0.9, -0.9, 2.2 / 255, 255.0)
+    st = _lib.stream_of(xg)
+    outs = []
+    for use_lut in (False, True):
+        oc = torch.full((n, ho + 2, wo + 2, cp), 77, dtype=torch.int8, device=gpu)
+        code = _lib.CodeOut(_lib.ptr(oc), cp, 1, ho + 2, wo + 2, 0.2, 1.7 / 255, 255.0)
+        if use_lut:
+            lut = torch.empty((c, 256), dtype=torch.int8, device=gpu)
+            _lib.call("qnn_bn_code_lut", ctypes.byref(bn), c, 1, ctypes.byref(code), _lib.ptr(lut), st)
+            _lib.call("qnn_dwconv_fused_lut", _lib.ptr(xg), n, h, w, pad, hp, wp, cp, c, _lib.ptr(wt), k, k, s, s,
+                      ho, wo, xmin, xs, None, ctypes.byref(bn), _lib.ptr(lut), ctypes.byref(code), st)
+        else:
+            _lib.call("qnn_dwconv_fused_generic", _lib.ptr(xg), n, h, w, pad, hp, wp, cp, c, _lib.ptr(wt), k, k, s,
+                      s, ho, wo, xmin, xs, None, ctypes.byref(bn), 1, None, ctypes.byref(code), st)
+        torch.cuda.synchronize()
+        outs.append(oc)
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    assert bool((outs[1][:, 0] == 77).all()) and bool((outs[1][:, :, 0] == 77).all())
