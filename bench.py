@@ -27,7 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec, 8-bit ResNet-18 224×224 @1/2/4/8 GPU; % int8-MFMA roofline"
-ROUND = 5  # profiles/rNN_traffic_* from an earlier round measured other kernels: never cited as traffic
+ROUND = 6  # profiles/rNN_traffic_* from an earlier round measured other kernels: never cited as traffic
 PEAK_INT8_TOPS = 5000.0   # dense int8 MFMA, 256 CU x 2.4 GHz (MI355X_MICROARCH.md: 2x bf16 2.5 PF)
 PEAK_HBM_GBS = 8000.0
 
@@ -243,6 +243,17 @@ def in_graph_times(engine, reps):
     return out, full - rest, conv_alone
 
 
+def baseline_config(arch, depth, batch, world):
+    """Which BASELINE.json config this run measures (C1 is the reference's CPU case)."""
+    if arch == "mobilenet":
+        return "C4" if batch == 512 and world == 1 else None
+    if depth == 18 and batch == 128 and world == 1:
+        return "C2"
+    if depth == 50 and batch == 256:
+        return "C3" if world == 1 else "C5" if world == 8 else f"C5 shape at {world} GPUs"
+    return None
+
+
 def model_name(arch, depth):
     return "mobilenet" if arch == "mobilenet" else f"resnet{depth}"
 
@@ -316,18 +327,28 @@ def main():
     per_kernel, conv_ms_per_fwd, conv_alone_ms = in_graph_times(engine, reps=max(10, args.steps))
     launches = engine.num_launches
 
-    module_ips = None
+    module_ips = per_module_ips = None
     if args.module_path and world == 1:
-        with torch.no_grad():
-            x = engine.input.clone()
-            for _ in range(2):
-                model(x)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(max(2, args.steps // 4)):
-                model(x)
-            torch.cuda.synchronize()
-            module_ips = args.batch * max(2, args.steps // 4) / (time.perf_counter() - t1)
+        from qnn import dispatch
+
+        def time_model(n):  # the reference's caller: output = model(inputs) (main.py:359, no_grad :411)
+            with torch.no_grad():
+                x = engine.input.clone()
+                for _ in range(3):  # the dispatch builds its engine when a shape repeats
+                    model(x)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(n):
+                    model(x)
+                torch.cuda.synchronize()
+                return args.batch * n / (time.perf_counter() - t1)
+
+        module_ips = time_model(max(5, args.steps))  # qnn/dispatch.py: the cached fused engine
+        old = dispatch.DISPATCH[0]
+        dispatch.DISPATCH[0] = "off"  # the per-module kernels (fp32 NCHW at every module boundary)
+        per_module_ips = time_model(max(2, args.steps // 4))
+        dispatch.DISPATCH[0] = old
+        dispatch.reset(model)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -351,6 +372,7 @@ def main():
             "config": {"workload": (f"resnet_quantized depth={args.depth}" if args.model == "resnet" else
                                     "mobilenet_quantized") + f" imagenet eval forward, fused int8 engine "
                                    f"(hipGraph), per-GPU batch {args.batch}",
+                       "baseline_config": baseline_config(args.model, args.depth, args.batch, world),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{world}", "model_gop_per_batch": round(total_ops / 1e9, 2)},
             "roofline": {"bound": "mfma",
@@ -371,6 +393,10 @@ def main():
                        "kernel_ms_source": "in-graph: each launch kind captured as its own hipGraph in plan order, "
                                            "replayed between HIP events (bench.in_graph_times)"},
             "module_path_images_per_s": None if module_ips is None else round(module_ips, 1),
+            "module_path_note": "the reference's unchanged caller, output = model(inputs) under no_grad "
+                                "(main.py:359/411): ResNet/MobileNet.forward runs a cached fused engine "
+                                "(qnn/dispatch.py, policy QNN_ENGINE_DISPATCH), bitwise the per-module path",
+            "per_module_images_per_s": None if per_module_ips is None else round(per_module_ips, 1),
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:

@@ -39,6 +39,16 @@ enum {
 int qnn_abi_version(void);
 const char* qnn_last_error(void);
 
+/* Device-side error word of the current device: bit QNN_DEVERR_PB_SPIN is raised by a
+ * persistent-band convolution wave (configurations 45-49, qnn_qconv2d_fwd_nchw_f32) that gave up
+ * one of its bounded hand-off waits -- that launch's outputs are then unreliable.  Reads the word
+ * into *flags (nullable) and clears it when clear != 0.  Synchronizes the device. */
+enum { QNN_DEVERR_PB_SPIN = 1 };
+int qnn_device_errors(uint32_t* flags, int clear);
+/* Test hook: the iteration bound of those waits (limit >= 0; 0 gives every wait up at once, so a
+ * test can force the error path); limit < 0 restores the default. */
+int qnn_debug_set_spin_limit(int limit);
+
 /* ---------------------------------------------------------------- quantizer */
 
 /* UniformQuantize.forward with a host-side range (quantize.py:159-160 -> :42-103,

@@ -501,31 +501,25 @@ __global__ void bn_code_lut_kernel(qnn_bn_params bn, int c, int relu, qnn_code_o
 // Block = (image, 256 channels): lane = 4-channel group, wave w sums pixels w, w+4, ...
 // (several loads in flight per lane), then wave 0 adds the four partial sums in a fixed
 // order and divides by hw (adaptive_avg_pool / AvgPool2d eval; deterministic order).
-__global__ __launch_bounds__(256) void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c,
-                                                            int tiled, float* out_f32, qnn_code_out c0) {
-  __shared__ float4 part[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, img = blockIdx.y;
-  const int g = blockIdx.x * 64 + lane, cg = c >> 2, ct = (c + 31) >> 5;
+// The classifier's avg-pool in the module path's summation order: torch's AvgPool2d kernel
+// (aten avg_pool2d_out_cuda_frame) sums each output's window from +0 in row-major order, one
+// fp32 add per tap, then divides once by the window size (count_include_pad), so one thread
+// per 4 channels adds the hw pixels in order and divides: the engine's pooled features, and
+// therefore its logits, are bitwise the module path's.
+__global__ __launch_bounds__(64) void avgpool_quant_kernel(const float* __restrict__ x, int n, int hw, int c,
+                                                           int tiled, float* out_f32, qnn_code_out c0) {
+  const int img = blockIdx.y;
+  const int g = blockIdx.x * 64 + threadIdx.x, cg = c >> 2, ct = (c + 31) >> 5;
+  if (g >= cg) return;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (g < cg) {
-#pragma unroll 4
-    for (int t = wave; t < hw; t += 4) {
-      const int64_t m = (int64_t)img * hw + t;
-      const float4 v = *reinterpret_cast<const float4*>(x + (tiled ? ctile_index(m, 4 * g, ct) : m * c + 4 * g));
-      s.x = s.x + v.x; s.y = s.y + v.y; s.z = s.z + v.z; s.w = s.w + v.w;
-    }
-  }
-  part[wave][lane] = s;
-  __syncthreads();
-  if (wave != 0 || g >= cg) return;
-  float4 t = part[0][lane];
-#pragma unroll
-  for (int k = 1; k < 4; ++k) {
-    const float4 p = part[k][lane];
-    t.x = t.x + p.x; t.y = t.y + p.y; t.z = t.z + p.z; t.w = t.w + p.w;
+#pragma unroll 7
+  for (int t = 0; t < hw; ++t) {
+    const int64_t m = (int64_t)img * hw + t;
+    const float4 v = *reinterpret_cast<const float4*>(x + (tiled ? ctile_index(m, 4 * g, ct) : m * c + 4 * g));
+    s.x = s.x + v.x; s.y = s.y + v.y; s.z = s.z + v.z; s.w = s.w + v.w;
   }
   const float d = (float)hw;
-  const float val[4] = {t.x / d, t.y / d, t.z / d, t.w / d};
+  const float val[4] = {s.x / d, s.y / d, s.z / d, s.w / d};
   if (out_f32)
     *reinterpret_cast<float4*>(out_f32 + (int64_t)img * c + 4 * g) = make_float4(val[0], val[1], val[2], val[3]);
   if (c0.ptr) put_code4(c0, img, 0, 0, 4 * g, val);
@@ -714,7 +708,7 @@ int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* 
   QNN_REQUIRE(x, "null input");
   const qnn_code_out c0 = code0 ? *code0 : none_code();
   QNN_REQUIRE(n < 65536, "batch >= 65536");
-  hipLaunchKernelGGL(avgpool_quant_kernel, dim3((unsigned)cdiv(c / 4, 64), (unsigned)n), dim3(256), 0,
+  hipLaunchKernelGGL(avgpool_quant_kernel, dim3((unsigned)cdiv(c / 4, 64), (unsigned)n), dim3(64), 0,
                      (hipStream_t)stream, x, n, hw, c, x_tiled, out_f32, c0);
   QNN_LAUNCH_CHECK("qnn_avgpool_quant");
   return QNN_OK;

@@ -1842,6 +1842,12 @@ extern "C" int qnn_qconv2d_fwd(const int8_t* x, const int8_t* wq, const qnn_conv
 extern "C" int qnn_qconv2d_fwd_nchw_f32(const float* x, int c, int h, int w, int pad, float neg_min, float scale,
                                         float qmax, const int8_t* wq, const qnn_conv_desc* desc,
                                         const qnn_epilogue* epi, int tile, qnn_stream_t stream) {
+  if (x && (((uintptr_t)x) & 15) != 0) {
+    // the band fill reads the fp32 input with scalar loads, but the launch checks share
+    // qnn_qconv2d_fwd's 16-byte rule: a misaligned view takes the caller's two-launch path
+    set_error("fp32 input not 16-byte aligned (two-launch path)");
+    return QNN_ERR_UNSUPPORTED;
+  }
   Params p;
   const int rc0 = fwd_args(x, wq, desc, epi, p);
   if (rc0 != QNN_OK) return rc0 == -1 ? QNN_OK : rc0;

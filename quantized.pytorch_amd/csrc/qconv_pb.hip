@@ -52,6 +52,10 @@ __device__ unsigned long long qnn_pb_stamps[1 << 19];
 #define PB_TS(v) ((void)0)
 #endif
 
+// the device error word (include/qnn.h qnn_device_errors): a global vector atomic OR, read and
+// cleared by the host
+__device__ unsigned qnn_dev_errors;
+
 namespace qnn {
 namespace pb {
 
@@ -87,6 +91,7 @@ struct Geo {
   int wstage;     // stage the weights through LDS (else each wave loads them from L2)
   int wsep;       // ... in a region of their own at wst_off (else in the band buffers, wst_off = 0)
   int wst_off;
+  int spin_max;   // bound of every hand-off wait (SPIN_MAX; qnn_debug_set_spin_limit for tests)
 };
 
 // q = m / D, r = m % D for 0 <= m < 2^24 (checked on the host): the float quotient is off by at
@@ -196,9 +201,16 @@ __device__ __forceinline__ void lds_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Every wait on a counter is bounded (~0.1-0.5 s): a protocol error then yields wrong outputs that
-// the bitwise tests catch, never a wave that spins until the process is killed
+// Every wait on a counter is bounded (~0.1-0.5 s): a protocol error then yields wrong outputs, never
+// a wave that spins until the process is killed -- and the wave that gave up raises
+// QNN_DEVERR_PB_SPIN in the device error word (qnn_device_errors), so a production forward learns
+// of it too, not only the bitwise tests
 constexpr int SPIN_MAX = 1 << 21;
+static int g_spin_max = SPIN_MAX;  // qnn_debug_set_spin_limit
+
+__device__ __forceinline__ void spin_timeout(int lane) {
+  if (lane == 0) atomicOr(&qnn_dev_errors, (unsigned)QNN_DEVERR_PB_SPIN);
+}
 
 // LDS counters (inline asm: the compiler's waitcnt pass must not order them behind the invisible
 // band DMA, and no compiler-visible access may move across them)
@@ -661,7 +673,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     if (can_issue()) issue_band(issued++), tile_since_issue = false;
     while (issued <= j) {  // this band's buffer waits for another wave's last tile of band j - 2
       publish();             // (never wait while holding unpublished pieces another wave may wait for)
-      for (int guard = 0; !can_issue() && guard < SPIN_MAX; ++guard) __builtin_amdgcn_s_sleep(2);
+      int guard = 0;
+      for (; !can_issue() && guard < g.spin_max; ++guard) __builtin_amdgcn_s_sleep(2);
+      if (guard >= g.spin_max && !can_issue()) spin_timeout(lane);
       issue_band(issued++);
       tile_since_issue = false;
     }
@@ -671,7 +685,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     if (published <= j) publish();
     {
       const int target = C::W * (j / 2 + 1);
-      for (int guard = 0; lds_get(&s_sync[j & 1]) < target && guard < SPIN_MAX; ++guard) __builtin_amdgcn_s_sleep(1);
+      int guard = 0;
+      for (; lds_get(&s_sync[j & 1]) < target && guard < g.spin_max; ++guard) __builtin_amdgcn_s_sleep(1);
+      if (guard >= g.spin_max && lds_get(&s_sync[j & 1]) < target) spin_timeout(lane);
     }
 #if QNN_STAMP
     PB_TS(tb);
@@ -767,7 +783,9 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
   // the bands other waves still need from this one
   while (issued < nb) {
     publish();
-    for (int guard = 0; !can_issue() && guard < SPIN_MAX; ++guard) __builtin_amdgcn_s_sleep(2);
+    int guard = 0;
+    for (; !can_issue() && guard < g.spin_max; ++guard) __builtin_amdgcn_s_sleep(2);
+    if (guard >= g.spin_max && !can_issue()) spin_timeout(lane);
     issue_band(issued++);
     tile_since_issue = false;
   }
@@ -905,6 +923,7 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
     return v ? atoi(v) : 1;
   }();
   g.wstage = wstage;
+  g.spin_max = g_spin_max;
   g.xf = nullptr;
   if (fin) {
     g.xf = fin->x;
@@ -976,6 +995,25 @@ static bool ok_k(const Params& p) {
 }  // namespace pb
 
 int pb_count() { return pb::NP; }
+
+extern "C" int qnn_device_errors(uint32_t* flags, int clear) {
+  unsigned v = 0;
+  if (int rc = hip_check(hipDeviceSynchronize(), "qnn_device_errors: synchronize")) return rc;
+  if (int rc = hip_check(hipMemcpyFromSymbol(&v, HIP_SYMBOL(::qnn_dev_errors), sizeof(v)), "qnn_device_errors"))
+    return rc;
+  if (clear && v) {
+    const unsigned z = 0;
+    if (int rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(::qnn_dev_errors), &z, sizeof(z)), "qnn_device_errors: clear"))
+      return rc;
+  }
+  if (flags) *flags = v;
+  return QNN_OK;
+}
+
+extern "C" int qnn_debug_set_spin_limit(int limit) {
+  pb::g_spin_max = limit < 0 ? pb::SPIN_MAX : limit;
+  return QNN_OK;
+}
 
 #if QNN_STAMP
 extern "C" int qnn_debug_stamps_pb(void* dst, size_t bytes) {

@@ -94,15 +94,20 @@ __device__ __forceinline__ QParams make_qparams(float neg_min, float scale, floa
 }
 
 // Clamped quotient clamp(RN((x + nm) / s), 0, qmax) of quant_code_fast for a pair, before the
-// final round.  quant_code_fast's |q0| < 2^20 select is not needed here: inside that range the
-// two are the same Markstein quotient; beyond it the corrected quotient q differs from q0 by at
-// most a few ulps of q0 (|r| <= ulp(q0) s, x finite: every epilogue input is a finite fp32 sum of
-// finite codes times finite scales), so it is also beyond [0, qmax] on the same side and clamps to
-// the same 0 or qmax (tests/test_quant_math.py, clamp-free form vs IEEE division out to 2^31).
+// final round.  q0 is clamped to [-2^20, 2^20] first (one v_med3 per element, in place of
+// quant_code_fast's |q0| < 2^20 select): inside that range the corrected quotient is the
+// Markstein one; beyond it the true quotient is beyond [0, qmax] on the same side as the clamped
+// q0, and the correction keeps it there (|r| <= ulp(q0) s for an unclamped q0; for a clamped one
+// r = t - 2^20 s has the sign of t), so it clamps to the same 0 or qmax.  Without the clamp a
+// finite t with t * inv overflowing (|t| > FLT_MAX * s, a tiny scale) made r = -inf and
+// q = fma(-inf, inv, inf) = NaN (tests/test_quant_math.py: the clamp-free and the clamped
+// forms against IEEE division, quotients out to overflow).
 __device__ __forceinline__ f2 qclamp2(f2 x, const QParams& p) {
   const f2 t = x + p.nm;
   const f2 inv = {p.inv, p.inv}, s = {p.s, p.s};
-  const f2 q0 = t * inv;
+  f2 q0 = t * inv;
+  q0.x = __builtin_amdgcn_fmed3f(q0.x, -1048576.0f, 1048576.0f);
+  q0.y = __builtin_amdgcn_fmed3f(q0.y, -1048576.0f, 1048576.0f);
   const f2 r = pfma(-q0, s, t);
   f2 q = pfma(r, inv, q0);
   q.x = __builtin_amdgcn_fmed3f(q.x, 0.0f, p.qmax);

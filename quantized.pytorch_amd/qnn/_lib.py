@@ -104,6 +104,8 @@ SIGNATURES = {
     "qnn_comm_destroy": [],
     "qnn_measure_stats_f32": [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr],
     "qnn_rangebn_stats_f32": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "qnn_device_errors": [c_ptr, c_int],
+    "qnn_debug_set_spin_limit": [c_int],
     "qnn_rangebn_f32": [c_ptr, c_ptr, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr, c_int, c_ptr],
 }
@@ -111,6 +113,16 @@ SIGNATURES = {
 
 class QnnLibraryError(RuntimeError):
     pass
+
+
+DEVERR_PB_SPIN = 1  # QNN_DEVERR_PB_SPIN
+
+
+def device_errors(clear=True):
+    """The device error word (include/qnn.h qnn_device_errors; synchronizes the device)."""
+    v = ctypes.c_uint32(0)
+    call("qnn_device_errors", ctypes.byref(v), 1 if clear else 0)
+    return v.value
 
 
 class QnnError(RuntimeError):

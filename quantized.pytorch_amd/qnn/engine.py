@@ -17,9 +17,11 @@ classifier's quantizer are one kernel.  The resulting fixed launch sequence is
 captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed.
 
 Numerics: identical op order to the reference everywhere except the fp32
-contraction itself (exact int32 + fp32 decomposition) and the avg-pool sum
-order, i.e. the same per-layer bar as the module path; whole-model outputs are
-held to the drift-calibrated end-to-end bar (tests/test_gpu_engine.py).
+contraction itself (exact int32 + fp32 decomposition), i.e. the same per-layer
+bar as the module path, and bitwise the module path itself, logits included (the
+avg-pool sums in torch's AvgPool2d order); whole-model outputs are held to the
+drift-calibrated end-to-end bar (tests/test_gpu_engine.py).  The reference's own
+forward reaches a cached engine through qnn/dispatch.py.
 
 Ranges are read once when the engine is built (eval ranges are constants; the
 'aciq' method's in-place `running_var += 1e-8` side effect (quantize.py:258) is
@@ -714,6 +716,9 @@ class Engine:
         with torch.cuda.graph(self.graph, stream=s):
             self._run_ops()
         torch.cuda.synchronize(self.dev)
+        errs = _lib.device_errors(clear=False)  # a persistent-band launch gave up a hand-off wait
+        if errs:
+            raise RuntimeError(f"qnn.Engine: device error word {errs:#x} after the warm-up forward (include/qnn.h)")
 
     def capture_subset(self, names):
         """A hipGraph of only the launches whose ABI name is in `names`, in plan order (for

@@ -16,6 +16,9 @@ for p in (REPO, PKG):
 # cost model's configuration instead (every configuration is checked on its own), and
 # tests/test_gpu_tiles.py::test_module_autotune_bitwise covers the autotune itself.
 os.environ.setdefault("QNN_MODULE_AUTOTUNE", "0")
+# The reference-forward dispatch to the fused engine (qnn/dispatch.py) is tested on its own
+# (tests/test_gpu_dispatch.py); elsewhere model(x) is the per-module path the tests check.
+os.environ.setdefault("QNN_ENGINE_DISPATCH", "off")
 
 
 def pytest_configure(config):

@@ -213,3 +213,107 @@ def test_sharded_engine_world2_device(gpu, tmp_path):
     assert got["logits"].shape == ref.shape
     ndiff = int((got["logits"] != ref).sum())
     assert ndiff == 0, f"{ndiff} gathered logits differ from the single-process engine"
+
+
+# ---------------------------------------------------------------- C5 at world 2
+# BASELINE.json configs[4] (C5): resnet_quantized depth=50, global batch 2048 sharded over 8 GPUs
+# (per-rank batch 256) with one RCCL gather of the logits.  One box has one GPU, so the same code
+# runs at world 2 (gloo, two ranks on cuda:0) at the C5 per-rank batch: each rank calibrates on
+# its shard, allreduce_calibration merges, build_engine plans the rank's b256 engine with rank 0's
+# autotuned tiles, ShardedInference gathers -- once with even shards (2 x 256) and once ragged
+# (256 + 255).  Reference: nn.DataParallel at main.py:342-343.
+C5_FIXTURE = "model_resnet50_imagenet"
+C5_CASES = (512, 511)  # global batches: even and ragged shards at the per-rank batch 256
+C5_CALIB = 6
+
+
+def _c5_calib_batches(rank, world):
+    from qnn import synthetic
+    from qnn.dist import shard_bounds
+    s, e = shard_bounds(C5_CALIB, world, rank)
+    return [synthetic.input_batch((C5_CALIB, 3, 224, 224), 700 + j)[s:e] for j in range(2)]
+
+
+def _c5_input(gb):
+    from qnn import synthetic
+    return synthetic.input_batch((gb, 3, 224, 224), 800 + gb)
+
+
+def _c5_worker(rank, world, port, out):
+    dist = _init(rank, world, port)
+    from conftest import load_fixture
+    from fixtures_util import build_model
+    from qnn.dist import ShardedInference, allreduce_calibration, build_engine, shard_bounds
+    dev = torch.device("cuda:0")
+    model, _ = build_model(load_fixture(C5_FIXTURE))
+    model = model.to(dev)
+    batches = _c5_calib_batches(rank, world)
+    _calibrate(model, batches, dev)
+    allreduce_calibration(model, samples=batches[0].shape[0])
+    res = {}
+    for gb in C5_CASES:
+        s, e = shard_bounds(gb, world, rank)
+        print(f"[c5 rank {rank}] global batch {gb}: building the b{e - s} engine", flush=True)
+        eng = build_engine(model, e - s)  # rank 0 autotunes, the other rank runs its tiles
+        runner = ShardedInference(eng, gb)
+        logits = runner(_c5_input(gb)[s:e].to(dev))
+        res[gb] = {"tiles": [k for k, _ in eng.tiles], "shard": (s, e),
+                   "logits": None if logits is None else logits.detach().cpu()}
+        if rank != 0:
+            assert logits is None
+        del runner, eng
+        torch.cuda.empty_cache()
+    if rank == 0:
+        res["state"] = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    torch.save(res, f"{out}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_sharded_engine_world2_c5_resnet50(gpu, tmp_path):
+    """C5's data path at world 2 and the C5 per-rank batch: the gathered logits of the sharded
+    engines equal, bitwise, one engine over the whole global batch built from the same merged
+    calibration (even and ragged shards)."""
+    from conftest import load_fixture
+    from fixtures_util import build_model
+    from qnn.dist import shard_bounds
+    from qnn.engine import Engine
+    out = str(tmp_path / "c5.pt")
+    _spawn(_c5_worker, (out,), timeout=800)
+    got = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+    assert [got[r][512]["shard"] for r in range(2)] == [(0, 256), (256, 512)]
+    assert [got[r][511]["shard"] for r in range(2)] == [(0, 256), (256, 511)]
+    # the merged calibration: rebuild each rank's own calibration here and merge it the same way
+    w = [b[0].shape[0] for b in (_c5_calib_batches(0, 2), _c5_calib_batches(1, 2))]
+    states = []
+    for r in range(2):
+        model, _ = build_model(load_fixture(C5_FIXTURE))
+        model = model.to(gpu)
+        _calibrate(model, _c5_calib_batches(r, 2), gpu)
+        states.append(model)
+    merged = states[0]
+    from qnn.quantize import QuantMeasure, RangeBN
+    with torch.no_grad():
+        for (n, m0), m1 in zip(merged.named_modules(), [m for _, m in states[1].named_modules()]):
+            names = (("running_min", "running_max", "running_mean", "running_var") if isinstance(m0, QuantMeasure)
+                     else ("running_mean", "running_var") if isinstance(m0, RangeBN) else ())
+            for k in names:
+                a, b = getattr(m0, k), getattr(m1, k)
+                a.copy_((a.double() * w[0] + b.double() * w[1]) / (w[0] + w[1]))
+                assert torch.equal(got[0]["state"][n + "." + k if n else k], a.cpu()), f"merged {n}.{k}"
+    del states
+    for gb in C5_CASES:
+        # rank 1 ran rank 0's tile configuration wherever it is built for its shard
+        t0, t1 = got[0][gb]["tiles"], got[1][gb]["tiles"]
+        assert len(t0) == len(t1)
+        eng = Engine(merged, batch=gb, autotune=False)  # the cost model's tiles: bitwise all the same
+        ref = eng(_c5_input(gb).to(gpu)).clone().cpu()
+        del eng
+        torch.cuda.empty_cache()
+        logits = got[0][gb]["logits"]
+        assert logits.shape == ref.shape == (gb, 1000)
+        ndiff = int((logits != ref).sum())
+        assert ndiff == 0, f"global batch {gb}: {ndiff} gathered logits differ from the single-process engine"
+        print(f"C5 world 2, global batch {gb} (shards {shard_bounds(gb, 2, 0)}, {shard_bounds(gb, 2, 1)}): "
+              f"gathered logits bitwise the single-process engine")

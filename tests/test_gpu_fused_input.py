@@ -92,3 +92,39 @@ def test_fused_input_falls_back(gpu):
     assert not fused
     ref, _ = _fwd(wrap, xg, False)
     assert torch.equal(y, ref)
+
+
+def test_fused_input_misaligned_view_falls_back(gpu):
+    """A contiguous fp32 input at a 4-byte (not 16-byte) offset: the one-launch entry declines it
+    (QNN_ERR_UNSUPPORTED) and the two-launch path runs, bitwise the same output."""
+    wrap, x = _layer(*CASES[0])
+    wrap, xg = wrap.to(gpu), x.to(gpu)
+    ref, _ = _fwd(wrap, xg, False)
+    buf = torch.empty(xg.numel() + 4, dtype=torch.float32, device=gpu)
+    xm = buf[1:1 + xg.numel()].view_as(xg)
+    xm.copy_(xg)
+    assert xm.is_contiguous() and xm.data_ptr() % 16 != 0
+    y, fused = _fwd(wrap, xm, True)
+    assert not fused
+    assert torch.equal(y, ref)
+
+
+def test_spin_timeout_raises_device_error(gpu):
+    """A persistent-band wave that gives up a bounded hand-off wait raises QNN_DEVERR_PB_SPIN in
+    the device error word (forced here by a spin bound of 0); with the default bound the word stays
+    clear and the output is the two-launch path's."""
+    wrap, x = _layer(*CASES[0])
+    wrap, xg = wrap.to(gpu), x.to(gpu)
+    ref, _ = _fwd(wrap, xg, False)
+    assert _lib.device_errors() == 0
+    _lib.call("qnn_debug_set_spin_limit", 0)
+    try:
+        _, fused = _fwd(wrap, xg, True)
+        assert fused
+        flags = _lib.device_errors()
+    finally:
+        _lib.call("qnn_debug_set_spin_limit", -1)
+    assert flags & _lib.DEVERR_PB_SPIN, f"device error word {flags:#x}"
+    y, fused = _fwd(wrap, xg, True)
+    assert fused and _lib.device_errors() == 0
+    assert torch.equal(y, ref)

@@ -70,6 +70,25 @@ int main(int argc, char** argv) {
     float q0 = t * inv, q = fmaf(fmaf(-q0, s, t), inv, q0);
     float fast = rintf(med3(q, 0.0f, 255.0f));
     if (memcmp(&fast, &ref, 4)) ++bad;
+    /* the product form (qnn_internal.h qclamp2): q0 clamped to +-2^20 first */
+    float q0c = med3(q0, -1048576.0f, 1048576.0f), qc = fmaf(fmaf(-q0c, s, t), inv, q0c);
+    float fc = rintf(med3(qc, 0.0f, 255.0f));
+    if (memcmp(&fc, &ref, 4)) ++bad;
+  }
+  /* t * inv overflowing: tiny scales (normal and subnormal), finite t up to FLT_MAX, either sign,
+     and infinite t; the unclamped form gives NaN there, the clamped one the IEEE code */
+  for (long it = 0; it < n / 16; ++it) {
+    float s = bits((uint32_t)(xr() % 0x0f000000u) + 1u);
+    float inv = 1.0f / s;
+    if (!isfinite(inv)) continue;
+    float t = bits((uint32_t)((xr() & 0x7fffff) | ((uint32_t)(200 + (int)(xr() % 55)) << 23)));
+    if ((it & 7) == 7) t = INFINITY;
+    if (xr() & 1) t = -t;
+    float ref = rintf(med3(t / s, 0.0f, 255.0f));
+    float q0 = t * inv;
+    float q0c = med3(q0, -1048576.0f, 1048576.0f), qc = fmaf(fmaf(-q0c, s, t), inv, q0c);
+    float fc = rintf(med3(qc, 0.0f, 255.0f));
+    if (memcmp(&fc, &ref, 4)) ++bad;
   }
   printf("%ld\n", bad);
   return 0;
@@ -79,9 +98,11 @@ int main(int argc, char** argv) {
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
 def test_clamp_free_quantizer_codes_are_ieee(tmp_path):
-    """qnn_internal.h qclamp2 without a clamp of x + nm before the Markstein quotient: the code
-    (quotient clamped to [0, 255], rounded half to even) equals the IEEE division's for every
-    finite quotient, including those far beyond 2^20 where q0 and the corrected q differ."""
+    """The Markstein quotient clamped to [0, 255] and rounded half to even equals the IEEE
+    division's code for every finite quotient, including those far beyond 2^20 where q0 and the
+    corrected q differ; and qnn_internal.h qclamp2's form (q0 clamped to +-2^20 first) does so
+    also where t * inv overflows (tiny scales, |t| up to FLT_MAX, infinite t), where the
+    unclamped correction would give fma(-inf, inv, inf) = NaN."""
     c = tmp_path / "cf.c"
     c.write_text(SRC_CLAMP)
     exe = tmp_path / "cf"
