@@ -1516,16 +1516,18 @@ static const CfgInfo XCFG[NX] = {
 static const int XKSP_BK[NX] = {0, 0, 0, 0, 64, 128};  // K-group configurations: their stage size
 
 // Whether configuration k is built for (and fits) this layer and epilogue kind
-static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1 + pb_count() + NX; }
+static int ncfg_all() { return NCFG + q16_count() + rb_count() + rbp_count() + dtab_count() + 1 + pb_count() + NX + rs_count(); }
 static int rb_first() { return NCFG + q16_count(); }
 static int rbp_first() { return NCFG + q16_count() + rb_count(); }
 static int dtab_first() { return rbp_first() + rbp_count(); }
 static int dhead_id() { return dtab_first() + dtab_count(); }  // configuration 44: the classifier head
 static int pb_first() { return dhead_id() + 1; }                 // configurations 45-49: persistent band
 static int xr_first() { return pb_first() + pb_count(); }         // configurations 50-55: extra ring tiles
+static int rs_first() { return xr_first() + NX; }                 // configurations 56-63: streamed resident band
 
 static bool cfg_ok(int k, const Params& p) {
   if (k >= ncfg_all()) return false;
+  if (k >= rs_first()) return rs_ok(k - rs_first(), p);
   if (k >= xr_first()) {
     const int x = k - xr_first();
     if (XKSP_BK[x] && (p.d.kpad / XKSP_BK[x]) % 2) return false;  // two K groups: an even stage count
@@ -1550,6 +1552,7 @@ static bool cfg_ok(int k, const Params& p) {
 // Estimated time (arbitrary units) of config k: rounds of resident blocks over the CUs,
 // each round as long as one block's padded MFMA work at that config's rate.
 static double cfg_cost(int k, const Params& p) {
+  if (k >= rs_first()) return rs_cost(k - rs_first(), p);
   const bool xr = k >= xr_first();  // the extra ring tiles: the ring's cost model below
   if (!xr && k >= pb_first()) return pb_cost(k - pb_first(), p);
   if (k == dhead_id()) return p.M <= 256 ? 0.0 : 1e30;  // measured: ahead of cfg 11 at b128 (6.4 vs 11.2 us), behind at b512
@@ -1587,6 +1590,7 @@ static int pick_cfg(const Params& p) {
 }
 
 static int launch_cfg(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s) {
+  if (k >= rs_first()) return rs_launch(k - rs_first(), x, w, p, s);
   if (k >= xr_first()) {
     switch (k - xr_first()) {
       case 0: return launch_ek<X0>(x, w, p, s);
@@ -1679,6 +1683,7 @@ extern "C" int qnn_conv_tile_count(void) { return ncfg_all(); }
 
 extern "C" const char* qnn_conv_tile_kernel(int k) {
   if (k < 0 || k >= ncfg_all()) return nullptr;
+  if (k >= rs_first()) return "qconv_rs_kernel";
   if (k >= xr_first()) return "qconv_kernel";
   if (k >= pb_first()) return "qconv_pb_kernel";
   if (k == dhead_id()) return "qconv_direct_kernel";
@@ -1701,7 +1706,8 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
   if (cfg) *cfg = k;
   int tbm, tbn;
-  if (k >= xr_first()) tbm = XCFG[k - xr_first()].bm, tbn = XCFG[k - xr_first()].bn;
+  if (k >= rs_first()) rs_tile(k - rs_first(), &tbm, &tbn);
+  else if (k >= xr_first()) tbm = XCFG[k - xr_first()].bm, tbn = XCFG[k - xr_first()].bn;
   else if (k >= pb_first()) pb_tile(k - pb_first(), &tbm, &tbn);
   else if (k == dhead_id()) tbm = 16, tbn = 64;
   else if (k >= dtab_first()) dtab_tile(k - dtab_first(), &tbm, &tbn);
@@ -1712,7 +1718,8 @@ extern "C" int qnn_conv_plan(const qnn_conv_desc* desc, const qnn_epilogue* epi,
   if (bm) *bm = tbm;
   if (bn) *bn = tbn;
   if (nblk)
-    *nblk = k >= xr_first() ? (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm))
+    *nblk = k >= rs_first() ? (int)rs_blocks(k - rs_first(), p)
+            : k >= xr_first() ? (int)(cdiv(p.M, tbn) * cdiv(p.d.cout, tbm))
             : k >= pb_first() ? (int)pb_blocks(k - pb_first(), p)
             : k == dhead_id() ? (int)dhead_blocks(p)
             : k >= dtab_first() ? (int)dtab_blocks(k - dtab_first(), p)
@@ -1762,10 +1769,11 @@ extern "C" int qnn_conv_occupancy(const qnn_conv_desc* desc, const qnn_epilogue*
   if (rc != QNN_OK) return rc;
   const int k = pick_cfg(p);
   QNN_REQUIRE(k >= 0, "tile configuration not built for this layer / epilogue kind");
-  QNN_REQUIRE(k >= rb_first() && k < xr_first(),
+  QNN_REQUIRE(k >= rb_first() && (k < xr_first() || k >= rs_first()),
               "occupancy is reported for the resident-band, direct-fragment and persistent-band configurations");
   Occ o{0, 0, 0};
-  const int r = k >= pb_first()    ? pb_launch(k - pb_first(), nullptr, nullptr, p, nullptr, &o)
+  const int r = k >= rs_first()    ? rs_launch(k - rs_first(), nullptr, nullptr, p, nullptr, &o)
+                : k >= pb_first()    ? pb_launch(k - pb_first(), nullptr, nullptr, p, nullptr, &o)
                 : k == dhead_id()    ? dhead_launch(nullptr, nullptr, p, nullptr, &o)
                 : k >= dtab_first()  ? dtab_launch(k - dtab_first(), nullptr, nullptr, p, nullptr, &o)
                 : k >= rbp_first() ? rbp_launch(k - rbp_first(), nullptr, nullptr, p, nullptr, &o)

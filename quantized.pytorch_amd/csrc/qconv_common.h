@@ -159,6 +159,14 @@ double direct_cost(int k, const Params& p);
 int64_t direct_blocks(int k, const Params& p);
 int direct_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
 
+// qconv_rb.hip's streamed resident-band configurations (the last ids, after the extra ring tiles)
+int rs_count();
+void rs_tile(int k, int* bm, int* bn);
+bool rs_ok(int k, const Params& p);
+double rs_cost(int k, const Params& p);
+int64_t rs_blocks(int k, const Params& p);
+int rs_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ = nullptr);
+
 // qconv_rbp.hip's two-team resident-band configurations (ids after the direct ones)
 int rbp_count();
 void rbp_tile(int k, int* bm, int* bn);

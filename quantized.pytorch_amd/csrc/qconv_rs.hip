@@ -1,0 +1,603 @@
+// Streamed resident-band int8 convolution on v_mfma_i32_16x16x64_i8 (configurations 56-61): the
+// eval forward of QConv2d (models/modules/quantize.py:314-349) for 3x3 layers whose whole-image
+// band fits LDS, bitwise the other configurations (SURVEY.md §0.5 decomposition, shared epilogue).
+#include "rb_common.h"
+
+namespace qnn {
+namespace rb {
+
+// ---------------------------------------------------------------- streamed resident band (rs)
+// qconv_rb_kernel's tile and main loop (one block per CU owns whole images x BM channels, the
+// band resident in LDS as 32-byte planes, each wave's weights straight into VGPRs), with the
+// block's serial phases taken off the K loop's critical path:
+// * the band arrives in CHUNKS of 2H planes (64H channels), in the order the K loop consumes
+//   them: the loop starts when chunk 0 has landed, and each wave issues its pieces of chunk c + 1
+//   during chunk c's first K steps, one per step, behind that step's weight refill (so the
+//   compiler's own weight waits -- vmcnt is in order -- have already covered a piece when its
+//   chunk begins; a raw s_barrier then publishes the chunk to the other waves);
+// * sum_valid(q'_x): each thread sums its band pixels' channels chunk by chunk at the chunk
+//   boundaries (v_dot4 against 1s) and publishes them after the last one (one more barrier), so
+//   only the 9-tap box sum remains for the epilogue;
+// * each wave DMAs the epilogue data of ITS OWN channels (per-channel vectors, border table, the
+//   EK_LUT code table rows) during the last chunk's K steps and waits only for its own DMA: no
+//   workgroup barrier after the K loop, so the waves of a SIMD drift apart and one's epilogue runs
+//   beside the other's MFMAs;
+// * NP = 2 passes: a wave computes its pixel tiles in two halves (K loop, epilogue, K loop,
+//   epilogue), the second pass's first weights fetched before the first epilogue; with PRIO the
+//   first wave of each SIMD runs at s_setprio 1, so the pair staggers and each epilogue overlaps
+//   the partner's MFMAs (MI355X_MICROARCH: the matrix pipe and VALU issue are shared per SIMD).
+// The DMAs are inline asm (global_load_lds with m0), invisible to the compiler's waitcnt pass:
+// it neither drains them before the band reads nor miscounts its weight waits (invisible older
+// VMEM ops only make a counted wait stricter).  Outputs are bitwise those of every other
+// configuration (the same contraction and epilogue arithmetic).
+#if QNN_STAMP
+__device__ unsigned long long qnn_rs_stamps[1 << 18];
+#endif
+
+template <class C, int EK, int H, int NP, int PRIO>
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4))) void qconv_rs_kernel(
+    const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
+  constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
+  constexpr int CPL = 2 * H;  // planes per chunk
+  constexpr int NPT = 4;      // band pixels per thread (geometry: nbp <= NPT * NT)
+  constexpr int TN0 = NP == 1 ? TN : (TN + 1) / 2;
+  constexpr int CW = 16 * TM;  // this wave's channels
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+
+  const qnn_conv_desc& d = p.d;
+  const qnn_epilogue& e = p.e;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+#if QNN_STAMP
+  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0, ts6 = 0;
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+  RB_TS(ts0);
+#endif
+
+  // ---- XCD-aware bijective block -> (band, channel tile) map, channel tiles fastest
+  const int nby = (d.cout + BM - 1) / BM;
+  const int nblk = g.nbands * nby;
+  int t;
+  {
+    const int bb = blockIdx.x, xcd = bb & 7, q = nblk >> 3, r = nblk & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bb >> 3);
+  }
+  const int band = t / nby;
+  const int c0 = (t - band * nby) * BM;
+  const int r0 = band * g.rows;
+  const int nrows_all = d.n * d.ho;
+  const int R0 = (r0 / d.ho) * d.hp + (r0 % d.ho) * d.sh;
+  const int rows_in = d.n * d.hp;
+
+  // ---- band DMA (inline asm): piece (r, v) = 1 KiB of plane v, band pixels [32r, 32r + 32),
+  // lane i pixel + (i >> 1), half i & 1; past the band the last pixel again (identical bytes)
+  auto issue_piece = [&](int r, int v) {
+    r = r < g.ppp ? r : g.ppp - 1;
+    int b = r * 32 + (lane >> 1);
+    b = b < g.nbp ? b : g.nbp - 1;
+    const int br = b / g.wb, cc = b - br * g.wb;
+    const int col = g.s2 ? (cc < g.we ? 2 * cc : 2 * (cc - g.we) + 1) : cc;
+    int row = R0 + br;
+    row = row < rows_in ? row : rows_in - 1;  // past the batch: feeds only pixels never stored
+    const uint32_t off =
+        cc >= d.wp ? (uint32_t)d.zero_off : (uint32_t)((row * d.wp + col) * d.cp + 32 * v + 16 * (lane & 1));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(smem + v * g.pl + r * 1024));
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(dst), "v"(off), "s"(x) : "memory", "m0");
+  };
+  const int nchunk = g.npl / CPL;
+  const int npr = (g.ppp + W - 1) / W;  // this wave's ranges r = wave + W*k of each plane
+  const int ppc = npr * CPL;             // its pieces of one chunk
+  auto issue_chunk = [&](int c, int i) { issue_piece(wave + W * (i / CPL), c * CPL + i % CPL); };
+  for (int i = 0; i < ppc; ++i) issue_chunk(0, i);
+
+  // ---- the epilogue data of this wave's channels cw0 .. cw0 + CW (qconv_common.h stage_epi's
+  // layout), as jobs: per vector / table array one 4-byte-per-lane DMA per 64 channels, then the
+  // EK_LUT code-table rows (1 KiB = 4 rows per 16-byte-per-lane DMA)
+  const bool lut_on = EK == EK_LUT && g.lut;
+  int8_t* const epi = smem + p.epi_off;
+  const int cw0 = wm * CW;
+  const int cmax = d.cout - 1;
+  constexpr int VJ = (CW + 63) / 64;  // DMAs per array
+  const int nvec = (EK != EK_NCHW && e.bn_mean) ? 7 : 3;
+  const int narr = nvec + e.nclass + (EK == EK_GEN ? 4 * e.nres : 0);
+  const int nvj = narr * VJ;
+  const int njobs = nvj + (lut_on ? CW / 4 : 0);
+  auto epi_job = [&](int k) {
+    if (k < nvj) {
+      const int v = k / VJ, kk = k - v * VJ;
+      const int arr = v < nvec ? v : 7 + (v - nvec);
+      const int cl = cw0 + 64 * kk + lane;  // local channel of this lane
+      int c = c0 + cl;
+      c = c < cmax ? c : cmax;
+      const float* src;
+      switch (arr) {
+        case 0: src = e.sxsw; break;
+        case 1: src = e.sxbw; break;
+        case 2:  // no bias: zeros from the input's 128-byte zero page
+          if (!e.bias) {
+            src = reinterpret_cast<const float*>(x + d.zero_off);
+            c = lane & 31;
+          } else {
+            src = e.bias;
+          }
+          break;
+        case 3: src = e.bn_mean; break;
+        case 4: src = e.bn_sq; break;
+        case 5: src = e.bn_wq; break;
+        case 6: src = e.bn_bq; break;
+        default:
+          if (arr - 7 < e.nclass) {
+            src = e.table + (int64_t)(arr - 7) * d.cout;
+          } else {
+            const int lk = arr - 7 - e.nclass, l = lk >> 2, k4 = lk & 3;
+            const qnn_res_link& rl = e.res[l];
+            src = k4 == 0 ? rl.mean : k4 == 1 ? rl.sq : k4 == 2 ? rl.wq : rl.bq;
+          }
+          break;
+      }
+      const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(epi + 4 * (arr * BM + cw0 + 64 * kk)));
+      if (CW % 64 == 0 || 64 * kk + lane < CW)  // lanes past this wave's channels write nothing
+        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(src + c) : "memory", "m0");
+    } else if (k < njobs) {
+      const int jl = k - nvj;  // rows cw0 + 4 jl .. + 3
+      int c = c0 + cw0 + 4 * jl + (lane >> 4);
+      c = c < cmax ? c : cmax;
+      const int8_t* src = e.lut + (int64_t)c * 256 + 16 * (lane & 15);
+      const uint32_t m =
+          __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(epi + 4 * (7 + e.nclass) * BM + 256 * (cw0 + 4 * jl)));
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+    }
+  };
+
+  // ---- the lane's band offset of output tile j (block pixel (wn*TN + j)*16 + (lane & 15); past
+  // the block it stands in for the block's last pixel and is never stored)
+  const int npx_blk = __builtin_amdgcn_readfirstlane((r0 + g.rows <= nrows_all ? g.rows : nrows_all - r0) * d.wo);
+  auto band_px = [&](int j) {
+    int q = (wn * TN + j) * 16 + (lane & 15);
+    q = q < npx_blk ? q : npx_blk - 1;
+    const int rr = q / d.wo, col = q - rr * d.wo;
+    const int r = r0 + rr, n = r / d.ho, ho = r - n * d.ho;
+    return (n * d.hp + ho * d.sh - R0) * g.wb + col;  // band pixel of tap (0, 0)
+  };
+  const int lsel = (lane >> 5) * g.pl + 16 * ((lane >> 4) & 1);
+
+  // ---- weights: rows c0 + cw0 + 16*i + (lane & 15), K bytes 16*(lane >> 4) of each step
+  const int8_t* wblk = w + (int64_t)c0 * d.kpad;
+  uint32_t aoff[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int row = cw0 + 16 * i + (lane & 15);
+    row = c0 + row < d.cout_pad ? row : d.cout_pad - 1 - c0;
+    aoff[i] = (uint32_t)(row * d.kpad + 16 * (lane >> 4));
+  }
+  const int KS = (d.cp / 64) * p.taps;
+  const int SPC = H * p.taps;  // K steps per chunk
+  struct Cur {
+    int t, tr, tc, gp, h;
+  };
+  auto advance = [&](Cur& c) {
+    if (++c.h == H) {
+      c.h = 0;
+      if (++c.tc == d.kw) c.tc = 0, ++c.tr;
+      if (++c.t == p.taps) c.t = 0, c.tr = 0, c.tc = 0, ++c.gp;
+    }
+  };
+  auto kbytes = [&](const Cur& c) { return c.t * d.cp + 64 * (H * c.gp + c.h); };
+  v4i fa[DA][TM];
+  Cur cl = {0, 0, 0, 0, 0};
+  auto load_a = [&](v4i (&dst)[TM]) {
+    const int8_t* base = wblk + kbytes(cl);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const v4i*>(base + aoff[i]);
+    if (H * cl.gp + cl.h < d.cp / 64 - 1 || cl.t < p.taps - 1 || cl.h < H - 1) advance(cl);  // clamp at the last step
+  };
+  auto preload = [&] {
+    cl = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
+  };
+  preload();
+
+  // LDS constants
+  int* s_tap = reinterpret_cast<int*>(smem + g.tap_off);
+  int* s_hc = reinterpret_cast<int*>(smem + g.cls_off);
+  int* s_ps = reinterpret_cast<int*>(smem + g.psum_off);
+  if (tid < p.taps) {
+    const int tr = tid / d.kw, tc = tid - tr * d.kw;
+    s_tap[tid] = tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc);
+  }
+  for (int i = tid; i < d.ho + d.wo; i += NT) s_hc[i] = i < d.ho ? p.e.hcls[i] * p.e.nwc : p.e.wcls[i - d.ho];
+
+  // channel sums of this thread's band pixels, accumulated chunk by chunk; published (one more
+  // barrier) once the last chunk is summed
+  int psum[NPT];
+#pragma unroll
+  for (int u = 0; u < NPT; ++u) psum[u] = 0;
+  auto sum_chunk = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int b = tid + NT * u;
+      if (b < g.nbp) {
+        int sm[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int vv = 0; vv < CPL; ++vv) {
+          const int8_t* pp = smem + (c * CPL + vv) * g.pl + 32 * b;
+          const v4i a = *reinterpret_cast<const v4i*>(pp);
+          const v4i cc = *reinterpret_cast<const v4i*>(pp + 16);
+          sm[0] = __builtin_amdgcn_sdot4(a.x, 0x01010101, sm[0], false);
+          sm[1] = __builtin_amdgcn_sdot4(a.y, 0x01010101, sm[1], false);
+          sm[2] = __builtin_amdgcn_sdot4(a.z, 0x01010101, sm[2], false);
+          sm[3] = __builtin_amdgcn_sdot4(a.w, 0x01010101, sm[3], false);
+          sm[0] = __builtin_amdgcn_sdot4(cc.x, 0x01010101, sm[0], false);
+          sm[1] = __builtin_amdgcn_sdot4(cc.y, 0x01010101, sm[1], false);
+          sm[2] = __builtin_amdgcn_sdot4(cc.z, 0x01010101, sm[2], false);
+          sm[3] = __builtin_amdgcn_sdot4(cc.w, 0x01010101, sm[3], false);
+        }
+        psum[u] += (sm[0] + sm[1]) + (sm[2] + sm[3]);
+      }
+    }
+    if (c == nchunk - 1) {
+#pragma unroll
+      for (int u = 0; u < NPT; ++u)
+        if (tid + NT * u < g.nbp) s_ps[tid + NT * u] = psum[u];
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+
+  // chunk 0 (this wave's pieces, then every wave's) and the LDS constants
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((DA - 1) * TM) : "memory");
+  sum_chunk(0);
+  if (PRIO && wave < W / 2) __builtin_amdgcn_s_setprio(1);
+#if QNN_STAMP
+  RB_TS(ts1);
+#endif
+
+  const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+  const int HoWo = d.ho * d.wo;
+  const int lm = r0 * d.wo + npx_blk - 1;  // the block's last pixel (stand-in of slots past it)
+  const int ln = lm / HoWo, lho = (lm - ln * HoWo) / d.wo, lwo = lm - ln * HoWo - lho * d.wo;
+
+  // ---- one pass: the K loop over tiles J0 .. J0 + TNP of this wave, then their epilogue
+  auto pass = [&](auto tnc, auto j0c) {
+    constexpr int TNP = decltype(tnc)::value, J0 = decltype(j0c)::value;
+    constexpr bool FIRST = J0 == 0, LAST = J0 + TNP == TN;
+    using CP = Cfg<C::WGM, C::WGN, TM, TNP, DA, 1>;
+    int pb[TNP];
+#pragma unroll
+    for (int j = 0; j < TNP; ++j) pb[j] = band_px(J0 + j) * 32 + lsel;
+    v4i acc[TM][TNP];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TNP; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+
+    Cur cc = {0, 0, 0, 0, 0};
+    int chunk = 0, bg = 0;  // (first pass) current chunk; background jobs issued in it
+    auto background = [&] {
+      if constexpr (FIRST) {
+        if (chunk + 1 < nchunk) {
+          if (bg < ppc) issue_chunk(chunk + 1, bg++);
+        } else {
+          if (bg < njobs) epi_job(bg++);
+          if (bg < njobs) epi_job(bg++);
+          if (bg < njobs) epi_job(bg++);
+        }
+      }
+    };
+    auto step = [&](auto slotc) {
+      constexpr int SL = decltype(slotc)::value;
+      const int dt = cc.tr * g.wb + (g.s2 ? (cc.tc & 1) * g.we + (cc.tc >> 1) : cc.tc);
+      const int boff = (2 * (H * cc.gp + cc.h)) * g.pl + 32 * dt;
+      v4i fb[TNP];
+#pragma unroll
+      for (int j = 0; j < TNP; ++j) {
+        v4i r;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(pb[j] + boff));
+        fb[j] = r;
+      }
+      static_for<TNP>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        lds_wait<TNP - 1 - j>();
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[SL][i], fb[j], acc[i][j], 0, 0, 0);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      load_a(fa[(SL + DA - 1) % DA]);
+      background();
+      advance(cc);
+    };
+#pragma nounroll
+    for (int k0 = 0; k0 < KS; k0 += DA) {
+      if constexpr (FIRST) {
+        if (k0 > 0 && k0 % SPC == 0) {  // chunk boundary: this wave's pieces landed (counted), then every wave's
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * TM) : "memory");
+          asm volatile("s_barrier" ::: "memory");
+          ++chunk;
+          bg = 0;
+          sum_chunk(chunk);
+        }
+      }
+      step(std::integral_constant<int, 0>{});
+      if constexpr (DA > 1) step(std::integral_constant<int, 1>{});
+      if constexpr (DA > 2) step(std::integral_constant<int, 2>{});
+      if constexpr (DA > 3) step(std::integral_constant<int, 3>{});
+    }
+#if QNN_STAMP
+    if (FIRST) RB_TS(ts2);
+#endif
+    if constexpr (FIRST) {
+      while (bg < njobs) epi_job(bg++);  // (a last chunk shorter than the jobs)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's epilogue data, the clamped tail weights
+    }
+    if constexpr (!LAST) preload();  // the next pass's first weights, ahead of this epilogue's stores
+#if QNN_STAMP
+    if (FIRST) RB_TS(ts3);
+#endif
+    int sumq[TNP];
+#pragma unroll
+    for (int j = 0; j < TNP; ++j) {
+      sumq[j] = 0;
+      const int b0 = (pb[j] - lsel) >> 5;
+      int tr = 0, tc = 0;
+      for (int tt = 0; tt < p.taps; ++tt) {
+        sumq[j] += s_ps[b0 + tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc)];
+        if (++tc == d.kw) tc = 0, ++tr;
+      }
+    }
+#if QNN_STAMP
+    if (FIRST) RB_TS(ts5);
+#endif
+    int cq = (wn * TN + J0) * 16 + (lane & 15);
+    int cm = r0 * d.wo + (cq < npx_blk ? cq : npx_blk - 1);
+    int cn = cm / HoWo, cho = (cm - cn * HoWo) / d.wo, cwo = cm - cn * HoWo - cho * d.wo;
+    auto pixel = [&](int j, q16::Pix& P, int& pc) {
+      if (j > 0) {
+        cq += 16;
+        cwo += 16;
+        while (cwo >= d.wo) {
+          cwo -= d.wo;
+          if (++cho == d.ho) cho = 0, ++cn;
+        }
+      }
+      P.ok = cq < npx_blk;
+      P.m = P.ok ? r0 * d.wo + cq : lm;
+      P.n = P.ok ? cn : ln;
+      P.ho = P.ok ? cho : lho;
+      P.wo = P.ok ? cwo : lwo;
+      pc = s_hc[P.ho] + s_hc[d.ho + P.wo];
+    };
+    if (EK == EK_LUT && g.lut && c0 + BM <= d.cout && c0 + BM <= e.code0_cp) {
+      const float* s_f = reinterpret_cast<const float*>(epi);
+      const int8_t* s_lut = epi + 4 * (7 + e.nclass) * BM;
+      const int gq = lane >> 4;
+      float4 sw[TM], bw[TM], bi[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cl_ = cw0 + 16 * i + 4 * gq;
+        sw[i] = *reinterpret_cast<const float4*>(s_f + cl_);
+        bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cl_);
+        bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl_);
+      }
+#pragma unroll
+      for (int j = 0; j < TNP; ++j) {
+        q16::Pix P;
+        int pc;
+        pixel(j, P, pc);
+        int8_t* op = e.out_code0 +
+                     (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp + P.wo + e.code0_pad) * e.code0_cp +
+                     c0 + cw0 + 4 * gq;
+        const float* tp = s_f + (7 + pc) * BM + cw0 + 4 * gq;
+        const f2 p2 = {(float)sumq[j], (float)sumq[j]};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float4 tb = *reinterpret_cast<const float4*>(tp + 16 * i);
+          const v4i& a = acc[i][j];
+          const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
+          const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
+                        (f2){bi[i].x, bi[i].y};
+          const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
+                        (f2){bi[i].z, bi[i].w};
+          const f2 q0 = qclamp2(v0, bnp) + MAGIC_U8, q1 = qclamp2(v1, bnp) + MAGIC_U8;
+          const int8_t* lp = s_lut + (cw0 + 16 * i + 4 * gq) * 256;
+          const int b0_ = (uint8_t)lp[__float_as_uint(q0.x) & 255u];
+          const int b1 = (uint8_t)lp[256 + (__float_as_uint(q0.y) & 255u)];
+          const int b2 = (uint8_t)lp[512 + (__float_as_uint(q1.x) & 255u)];
+          const int b3 = (uint8_t)lp[768 + (__float_as_uint(q1.y) & 255u)];
+          *reinterpret_cast<int*>(op + 16 * i) = b0_ | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        }
+      }
+    } else {
+      q16::epilogue_rb<CP, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
+    }
+  };
+  pass(std::integral_constant<int, TN0>{}, std::integral_constant<int, 0>{});
+  if constexpr (NP > 1) pass(std::integral_constant<int, TN - TN0>{}, std::integral_constant<int, TN0>{});
+#if QNN_STAMP
+  RB_TS(ts6);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  RB_TS(ts4);
+  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && blockIdx.x < (1 << 18) / (8 * W)) {
+    unsigned long long* o = qnn_rs_stamps + ((size_t)blockIdx.x * W + wave) * 8;
+    o[0] = rt0; o[1] = rt1; o[2] = ts1 - ts0; o[3] = ts2 - ts1; o[4] = ts3 - ts2; o[5] = ts5 - ts3;
+    o[6] = ts6 - ts5; o[7] = ts4 - ts6;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------- rs host side
+// LDS of an rs block (band + sums + taps + classes, then the epilogue data, the EK_LUT code table
+// when it fits) and the geometry checks the streamed chunks need; a negative status if the layer
+// does not fit.
+template <class C, int EK, int H>
+static int rs_plan(const Params& p, Params& q, Geo& g) {
+  const int main = geometry(p, C::BM, C::BN, C::W, 1, 0, g);
+  if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
+  const int cpl = 2 * H, spc = H * p.taps;
+  const int ppc = (int)cdiv(g.ppp, C::W) * cpl;
+  if (g.npl % cpl || spc % C::DA || ppc + C::DA - 1 > spc || g.nbp > 4 * C::NT)
+    return arg_error("tile configuration not built for this layer / epilogue kind");
+  q = p;
+  int epi = epi_bytes(p, C::BM);
+  g.lut = 0;
+  if (EK == EK_LUT && main + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
+  if (main + epi > LDS_MAX) return arg_error("tile configuration not built for this layer / epilogue kind");
+  q.epi_early = 1, q.epi_off = main, q.scr_off = 0;
+  return main + epi;
+}
+
+template <class C, int EK, int H, int NP, int PRIO>
+static int rs_launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  auto kern = qconv_rs_kernel<C, EK, H, NP, PRIO>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+  if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  Geo g;
+  Params q;
+  const int lds = rs_plan<C, EK, H>(p, q, g);
+  if (lds < 0) return lds;
+  const int nblk = g.nbands * (int)cdiv(p.d.cout, C::BM);
+  if (occ) {
+    int n = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, C::NT, lds);
+    if (e != hipSuccess) return hip_check(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    occ->blocks_per_cu = n, occ->lds = lds, occ->grid = nblk;
+    return QNN_OK;
+  }
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(C::NT), lds, s, x, w, q, g);
+  return QNN_OK;
+}
+
+// the general chain spills beside more than 16 accumulator tiles (per pass): not built
+template <class C, int NP>
+constexpr bool rs_gen_ok() { return C::TM * ((C::TN + NP - 1) / NP) <= 16; }
+
+template <class C, int H, int NP, int PRIO>
+static int rs_launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  if (p.d.cp == 64 && H != 1) return arg_error("tile configuration not built for this layer / epilogue kind");
+  switch (epi_kind(p.e)) {
+    case EK_NCHW: return rs_launch_k<C, EK_NCHW, H, NP, PRIO>(x, w, p, s, occ);
+    case EK_LUT: return rs_launch_k<C, EK_LUT, H, NP, PRIO>(x, w, p, s, occ);
+    case EK_BNCODE: return rs_launch_k<C, EK_BNCODE, H, NP, PRIO>(x, w, p, s, occ);
+    default:
+      if constexpr (!rs_gen_ok<C, NP>()) return arg_error("tile configuration not built for this layer / epilogue kind");
+      else return rs_launch_k<C, EK_GEN, H, NP, PRIO>(x, w, p, s, occ);
+  }
+}
+
+//   id  block (cout x px cols)  waves (each)    K order / passes
+//   0   256 x 208               8 (32 x 208)    H = 2, 1 pass           14x14 images (ResNet-50 layer 3, b256)
+//   1   256 x 208               8 (32 x 208)    H = 1, 1 pass
+//   2   256 x 208               8 (32 x 208)    H = 2, 2 passes, priority stagger
+//   3   256 x 208               8 (32 x 208)    H = 1, 2 passes, priority stagger
+//   4   256 x 208               8 (32 x 208)    H = 2, 2 passes
+//   5   256 x 224               8 (64 x 112)    H = 2, 2 passes, priority stagger
+//   6   256 x 112               8 (32 x 112)    H = 2, 2 passes, priority stagger   half 14x14 images (ResNet-18 layer 3, b128)
+//   7   256 x 112               8 (32 x 112)    H = 1, 1 pass
+using S0 = Cfg<8, 1, 2, 13, 3, 1>;
+using S2 = Cfg<4, 2, 4, 7, 3, 1>;
+using S4 = Cfg<8, 1, 2, 7, 3, 1>;
+constexpr int NS = 8;
+static const Info SINFO[NS] = {
+    {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f},
+    {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f}, {256, 112, 8, 1, 14, 1.10f}, {256, 112, 8, 1, 14, 1.10f},
+};
+
+template <int K, class F>
+static auto rs_dispatch(F&& f) {
+  if constexpr (K == 0) return f(S0{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+  else if constexpr (K == 1) return f(S0{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+  else if constexpr (K == 2) return f(S0{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+  else if constexpr (K == 3) return f(S0{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+  else if constexpr (K == 4) return f(S0{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{});
+  else if constexpr (K == 5) return f(S2{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+  else if constexpr (K == 6) return f(S4{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+  else return f(S4{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+}
+
+template <class C, int H, int NP>
+static bool rs_ok_h(const Params& p) {
+  if (p.d.cp == 64 && H != 1) return false;
+  Params q;
+  Geo g;
+  switch (epi_kind(p.e)) {
+    case EK_NCHW: return rs_plan<C, EK_NCHW, H>(p, q, g) >= 0;
+    case EK_LUT: return rs_plan<C, EK_LUT, H>(p, q, g) >= 0;
+    case EK_BNCODE: return rs_plan<C, EK_BNCODE, H>(p, q, g) >= 0;
+    default: return rs_gen_ok<C, NP>() && rs_plan<C, EK_GEN, H>(p, q, g) >= 0;
+  }
+}
+
+template <int K>
+static bool rs_ok_k(const Params& p) {
+  return rs_dispatch<K>([&](auto c, auto h, auto np, auto) { return rs_ok_h<decltype(c), h.value, np.value>(p); });
+}
+
+template <int K>
+static int rs_launch_kk(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  return rs_dispatch<K>([&](auto c, auto h, auto np, auto pr) {
+    return rs_launch_ek<decltype(c), h.value, np.value, pr.value>(x, w, p, s, occ);
+  });
+}
+
+}  // namespace rb
+
+int rs_count() { return rb::NS; }
+
+void rs_tile(int k, int* bm, int* bn) {
+  *bm = rb::SINFO[k].bm;
+  *bn = rb::SINFO[k].bn;
+}
+
+bool rs_ok(int k, const Params& p) {
+  using namespace rb;
+  switch (k) {
+    case 0: return rs_ok_k<0>(p);
+    case 1: return rs_ok_k<1>(p);
+    case 2: return rs_ok_k<2>(p);
+    case 3: return rs_ok_k<3>(p);
+    case 4: return rs_ok_k<4>(p);
+    case 5: return rs_ok_k<5>(p);
+    case 6: return rs_ok_k<6>(p);
+    case 7: return rs_ok_k<7>(p);
+    default: return false;
+  }
+}
+
+int64_t rs_blocks(int k, const Params& p) {
+  const rb::Info& f = rb::SINFO[k];
+  rb::Geo g;
+  if (rb::geometry(p, f.bm, f.bn, f.w, 1, 0, g) < 0) return 0;
+  return (int64_t)g.nbands * cdiv(p.d.cout, f.bm);
+}
+
+double rs_cost(int k, const Params& p) {
+  const rb::Info& f = rb::SINFO[k];
+  rb::Geo g;
+  if (rb::geometry(p, f.bm, f.bn, f.w, 1, 0, g) < 0) return 1e30;
+  const int64_t tiles = (int64_t)g.nbands * cdiv(p.d.cout, f.bm);
+  return (double)cdiv(tiles, NUM_CU) * f.bm * f.bn * (p.taps * p.d.cp) / f.rate;
+}
+
+int rs_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  using namespace rb;
+  switch (k) {
+    case 0: return rs_launch_kk<0>(x, w, p, s, occ);
+    case 1: return rs_launch_kk<1>(x, w, p, s, occ);
+    case 2: return rs_launch_kk<2>(x, w, p, s, occ);
+    case 3: return rs_launch_kk<3>(x, w, p, s, occ);
+    case 4: return rs_launch_kk<4>(x, w, p, s, occ);
+    case 5: return rs_launch_kk<5>(x, w, p, s, occ);
+    case 6: return rs_launch_kk<6>(x, w, p, s, occ);
+    default: return rs_launch_kk<7>(x, w, p, s, occ);
+  }
+}
+
+#if QNN_STAMP
+extern "C" int qnn_debug_stamps_rs(void* dst, size_t bytes) {
+  if (bytes > sizeof(::qnn::rb::qnn_rs_stamps)) bytes = sizeof(::qnn::rb::qnn_rs_stamps);
+  return hip_check(hipMemcpyFromSymbol(dst, HIP_SYMBOL(::qnn::rb::qnn_rs_stamps), bytes), "stamps");
+}
+#endif
+}  // namespace qnn

@@ -112,8 +112,9 @@ def test_fused_input_misaligned_view_falls_back(gpu):
 def test_spin_timeout_raises_device_error(gpu):
     """A persistent-band wave that gives up a bounded hand-off wait raises QNN_DEVERR_PB_SPIN in
     the device error word (forced here by a spin bound of 0); with the default bound the word stays
-    clear and the output is the two-launch path's."""
-    wrap, x = _layer(*CASES[0])
+    clear and the output is the two-launch path's.  Batch 24: every block walks several bands, so
+    its waves wait on one another's hand-offs."""
+    wrap, x = _layer(64, 64, 1, 24, 56, 56, False)
     wrap, xg = wrap.to(gpu), x.to(gpu)
     ref, _ = _fwd(wrap, xg, False)
     assert _lib.device_errors() == 0
