@@ -405,7 +405,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
 template <class C, int EK>
 static int plan_lds(const Params& p, Params& q, Geo& g) {
   const int main = geometry(p, C::BM, C::BN, C::W, C::BPC, 0, g);
-  if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
+  if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind"), -1;
   q = p;
   int epi = epi_bytes(p, C::BM);
   // EK_LUT: the 256-byte-per-channel code table beside the band when it fits (else evaluated)
@@ -416,12 +416,12 @@ static int plan_lds(const Params& p, Params& q, Geo& g) {
     q.epi_early = 1, q.epi_off = main;
     lds = main + epi;
   } else {  // staged after the loop over the band (the border classes past it stay)
-    if (epi > g.psum_off) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+    if (epi > g.psum_off) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)"), -1;
     q.epi_early = 0, q.epi_off = 0;
     lds = main;
   }
   q.scr_off = 0;
-  if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)");
+  if (lds > LDS_MAX) return arg_error("conv tile needs more than 160 KiB of LDS (too many border classes)"), -1;
   return lds;
 }
 
@@ -434,7 +434,7 @@ static int launch(const int8_t* x, const int8_t* w, const Params& p, hipStream_t
   Geo g;
   Params q;
   const int lds = plan_lds<C, EK>(p, q, g);
-  if (lds < 0) return lds;
+  if (lds < 0) return QNN_ERR_ARG;  // (plan_lds set the message)
   // natural occupancy: as many blocks per CU as registers and LDS allow
   const int nblk = g.nbands * (int)cdiv(p.d.cout, C::BM);
   if (occ) {

@@ -325,6 +325,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
     }
 #if QNN_STAMP
     if (FIRST) RB_TS(ts2);
+    else RB_TS(ts6);
 #endif
     if constexpr (FIRST) {
       while (bg < njobs) epi_job(bg++);  // (a last chunk shorter than the jobs)
@@ -345,9 +346,6 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
         if (++tc == d.kw) tc = 0, ++tr;
       }
     }
-#if QNN_STAMP
-    if (FIRST) RB_TS(ts5);
-#endif
     int cq = (wn * TN + J0) * 16 + (lane & 15);
     int cm = r0 * d.wo + (cq < npx_blk ? cq : npx_blk - 1);
     int cn = cm / HoWo, cho = (cm - cn * HoWo) / d.wo, cwo = cm - cn * HoWo - cho * d.wo;
@@ -410,16 +408,21 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
     } else {
       q16::epilogue_rb<CP, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
     }
+#if QNN_STAMP
+    if (FIRST) RB_TS(ts5);
+#endif
   };
   pass(std::integral_constant<int, TN0>{}, std::integral_constant<int, 0>{});
   if constexpr (NP > 1) pass(std::integral_constant<int, TN - TN0>{}, std::integral_constant<int, TN0>{});
 #if QNN_STAMP
-  RB_TS(ts6);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   RB_TS(ts4);
+  if (NP == 1) ts6 = ts4;
   const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0 && blockIdx.x < (1 << 18) / (8 * W)) {
     unsigned long long* o = qnn_rs_stamps + ((size_t)blockIdx.x * W + wave) * 8;
+    // prologue (chunk 0), pass-0 K loop, its epilogue-data wait, pass-0 epilogue (box sums
+    // included), pass-1 K loop, pass-1 epilogue + store drain
     o[0] = rt0; o[1] = rt1; o[2] = ts1 - ts0; o[3] = ts2 - ts1; o[4] = ts3 - ts2; o[5] = ts5 - ts3;
     o[6] = ts6 - ts5; o[7] = ts4 - ts6;
   }
@@ -428,21 +431,20 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
 
 // ---------------------------------------------------------------- rs host side
 // LDS of an rs block (band + sums + taps + classes, then the epilogue data, the EK_LUT code table
-// when it fits) and the geometry checks the streamed chunks need; a negative status if the layer
-// does not fit.
+// when it fits) and the geometry checks the streamed chunks need; -1 if the layer does not fit.
 template <class C, int EK, int H>
 static int rs_plan(const Params& p, Params& q, Geo& g) {
   const int main = geometry(p, C::BM, C::BN, C::W, 1, 0, g);
-  if (main < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
+  if (main < 0) return -1;
   const int cpl = 2 * H, spc = H * p.taps;
   const int ppc = (int)cdiv(g.ppp, C::W) * cpl;
   if (g.npl % cpl || spc % C::DA || ppc + C::DA - 1 > spc || g.nbp > 4 * C::NT)
-    return arg_error("tile configuration not built for this layer / epilogue kind");
+    return -1;
   q = p;
   int epi = epi_bytes(p, C::BM);
   g.lut = 0;
   if (EK == EK_LUT && main + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
-  if (main + epi > LDS_MAX) return arg_error("tile configuration not built for this layer / epilogue kind");
+  if (main + epi > LDS_MAX) return -1;
   q.epi_early = 1, q.epi_off = main, q.scr_off = 0;
   return main + epi;
 }
@@ -456,7 +458,7 @@ static int rs_launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStr
   Geo g;
   Params q;
   const int lds = rs_plan<C, EK, H>(p, q, g);
-  if (lds < 0) return lds;
+  if (lds < 0) return arg_error("tile configuration not built for this layer / epilogue kind");
   const int nblk = g.nbands * (int)cdiv(p.d.cout, C::BM);
   if (occ) {
     int n = 0;

@@ -53,7 +53,7 @@ def run(eng, idx, d, e, tile, reps):
     fn = getattr(lib, "qnn_debug_stamps_" + KERNEL)
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     W = 8
-    S = 16 if KERNEL == "rbp" else 8  # stamp slots per wave
+    S = 16 if KERNEL == "rbp" else 8  # stamp slots per wave (rb, rs: 8)
     n = min(nblk.value, (1 << 18) // (S * W))
     buf = np.zeros(n * W * S, dtype=np.uint64)
     assert fn(buf.ctypes.data, buf.nbytes) == 0
@@ -65,10 +65,17 @@ def report(tag, us, nblk, w):
     cyc = w[:, :, 2:8]
     mean = cyc.mean((0, 1))
     tot = cyc.sum(-1).mean()
-    names = (["band", "k-loop", "sums", "staging", "epi", "drain"] if KERNEL == "rb" else
-             ["chunk0", "k-loop", "sums", "epidata", "epi", "drain"])
+    names = {"rb": ["band", "k-loop", "sums", "staging", "epi", "drain"],
+             "rbp": ["chunk0", "k-loop", "sums", "epidata", "epi", "drain"],
+             "rs": ["chunk0", "k-loop0", "epiwait", "epi0", "k-loop1", "epi1+drain"]}[KERNEL]
     print(f"== {tag}: {us:.1f} us (stamped build), blocks={nblk}, wave-cycles {tot:.0f}: " +
           "  ".join(f"{a}={m:.0f} ({100 * m / tot:.1f}%)" for a, m in zip(names, mean)))
+    if KERNEL == "rs":  # the SIMD pairs: waves 0-3 (priority 1 in the PRIO configurations) vs 4-7
+        for tm in (0, 1):
+            c = cyc[:, 4 * tm:4 * tm + 4]
+            cum = np.cumsum(c.mean((0, 1)))
+            print(f"   waves {4 * tm}-{4 * tm + 3}: " + "  ".join(f"{a}={m:.0f}" for a, m in zip(names, c.mean((0, 1)))) +
+                  "   cumulative: " + " ".join(f"{x:.0f}" for x in cum))
     if KERNEL == "rbp":  # the two teams (waves 0-3 at priority 2, 4-7 at 0)
         for tm in (0, 1):
             c = cyc[:, 4 * tm:4 * tm + 4]
@@ -93,7 +100,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--tiles", nargs="*", type=int, default=None)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--kernel", choices=("rb", "rbp"), default="rb")
+    ap.add_argument("--kernel", choices=("rb", "rbp", "rs"), default="rb")
     ap.add_argument("--only3x3", default="")
     a = ap.parse_args()
     global KERNEL
