@@ -43,6 +43,9 @@ __device__ __forceinline__ void epilogue16(const Params& p, const v4i (&acc)[C::
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
   const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
   const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+  // two consumers calibrated on the same tensor hold the same range: their codes are equal
+  const bool same01 = e.out_code0 && e.code1_neg_min == e.code0_neg_min && e.code1_scale == e.code0_scale &&
+                      e.code1_qmax == e.code0_qmax;
   const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
   const bool has_res = EK == EK_GEN && e.residual != nullptr;
 #pragma unroll
@@ -113,13 +116,13 @@ __device__ __forceinline__ void epilogue16(const Params& p, const v4i (&acc)[C::
           const int64_t fi = e.f32_tiled ? ctile_index(P.m, c, p.ct) : (int64_t)P.m * d.cout + c;
           *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
         }
-        if (e.out_code0 && P.ok && c < e.code0_cp) {
-          const int k0 = cok ? pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8) : 0;
+        int k0 = 0;
+        if (e.out_code0 && cok) k0 = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+        if (e.out_code0 && P.ok && c < e.code0_cp)
           *reinterpret_cast<int*>(e.out_code0 + (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp +
                                                  P.wo + e.code0_pad) * e.code0_cp + c) = k0;
-        }
         if (e.out_code1 && P.ok && c < e.code1_cp) {
-          const int k1 = cok ? pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8) : 0;
+          const int k1 = !cok ? 0 : same01 ? k0 : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
           *reinterpret_cast<int*>(e.out_code1 + (((int64_t)P.n * e.code1_hp + P.ho + e.code1_pad) * e.code1_wp +
                                                  P.wo + e.code1_pad) * e.code1_cp + c) = k1;
         }
@@ -157,6 +160,9 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
   const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
   const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+  // two consumers calibrated on the same tensor hold the same range: their codes are equal
+  const bool same01 = e.out_code0 && e.code1_neg_min == e.code0_neg_min && e.code1_scale == e.code0_scale &&
+                      e.code1_qmax == e.code0_qmax;
   const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
   const bool has_res = EK == EK_GEN && e.residual != nullptr;
   const int nres = EK == EK_GEN ? e.nres : 0;
@@ -338,12 +344,11 @@ __device__ __forceinline__ void epilogue_rb(const Params& p, const v4i (&acc)[C:
           const int64_t fi = e.f32_tiled ? ctile_index(P.m, c, p.ct) : (int64_t)P.m * d.cout + c;
           *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
         }
-        if (e.out_code0 && c < e.code0_cp) {
-          const int k0 = cok ? pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8) : 0;
-          *reinterpret_cast<int*>(e.out_code0 + px0 + c) = k0;
-        }
+        int k0 = 0;
+        if (e.out_code0 && cok) k0 = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+        if (e.out_code0 && c < e.code0_cp) *reinterpret_cast<int*>(e.out_code0 + px0 + c) = k0;
         if (EK == EK_GEN && e.out_code1 && c < e.code1_cp) {
-          const int k1 = cok ? pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8) : 0;
+          const int k1 = !cok ? 0 : same01 ? k0 : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
           *reinterpret_cast<int*>(e.out_code1 + (((int64_t)P.n * e.code1_hp + P.ho + e.code1_pad) * e.code1_wp +
                                                  P.wo + e.code1_pad) * e.code1_cp + c) = k1;
         }

@@ -252,6 +252,9 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
     const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
     const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
     const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+    // two consumers calibrated on the same tensor hold the same range: their codes are equal
+    const bool same01 = e.out_code0 && e.code1_neg_min == e.code0_neg_min && e.code1_scale == e.code0_scale &&
+                        e.code1_qmax == e.code0_qmax;
     const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
     const CodeDst t0 = {e.out_code0, e.code0_cp, e.code0_pad, e.code0_hp, e.code0_wp};
     const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
@@ -413,7 +416,7 @@ __device__ __forceinline__ void epilogue(const Params& p, v16i (&acc)[C::TM][C::
             if (e.out_code0 && cok)
               k0[g] = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
             if (e.out_code1 && cok)
-              k1[g] = pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
+              k1[g] = same01 ? k0[g] : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
           }
         }
         const int ch = cb + 16 * fh;

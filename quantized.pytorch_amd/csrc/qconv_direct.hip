@@ -581,6 +581,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void qc
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
   const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
   const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+  const bool same01 = e.out_code0 && e.code1_neg_min == e.code0_neg_min && e.code1_scale == e.code0_scale &&
+                      e.code1_qmax == e.code0_qmax;
   const bool want_bn = e.out_bncode != nullptr;
   const float* tab_l = s_tab + ((bn ? 1 : 0) * CB + cl) * TSTR;  // this lane's rows of link 0
   const float* tab_b = s_tab + cl * TSTR;                           // ... of the RangeBN table
@@ -685,12 +687,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void qc
         const int64_t fi = e.f32_tiled ? ctile_index(m, c, p.ct) : (int64_t)m * d.cout + c;
         *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
       }
-      if (e.out_code0 && c < e.code0_cp) {
-        const int k0 = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+      int k0 = 0;
+      if (e.out_code0) k0 = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+      if (e.out_code0 && c < e.code0_cp)
         *reinterpret_cast<int*>(e.out_code0 + code_off(C, j, m, e.code0_hp, e.code0_wp, e.code0_pad, e.code0_cp)) = k0;
-      }
       if (e.out_code1 && c < e.code1_cp) {
-        const int k1 = pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
+        // two consumers calibrated on the same tensor hold the same range: their codes are equal
+        const int k1 = same01 ? k0 : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
         *reinterpret_cast<int*>(e.out_code1 + code_off(C, j, m, e.code1_hp, e.code1_wp, e.code1_pad, e.code1_cp)) = k1;
       }
     }

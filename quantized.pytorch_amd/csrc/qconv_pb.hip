@@ -330,6 +330,8 @@ __device__ __forceinline__ void gen_epilogue(const Params& p, const v4i (&acc)[C
   const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
   const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
   const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+  const bool same01 = e.out_code0 && e.code1_neg_min == e.code0_neg_min && e.code1_scale == e.code0_scale &&
+                      e.code1_qmax == e.code0_qmax;
   const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
   const f2 p2 = {(float)psq, (float)psq};
   const float* tp = s_f + (7 + pc) * BM;
@@ -431,11 +433,13 @@ __device__ __forceinline__ void gen_epilogue(const Params& p, const v4i (&acc)[C
       const int64_t fi = e.f32_tiled ? ctile_index(m, c, p.ct) : (int64_t)m * d.cout + c;
       *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
     }
-    if (e.out_code0 && c < e.code0_cp)
-      *reinterpret_cast<int*>(e.out_code0 + px0 + c) = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
-    if (e.out_code1 && c < e.code1_cp)
+    int k0 = 0;
+    if (e.out_code0) k0 = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+    if (e.out_code0 && c < e.code0_cp) *reinterpret_cast<int*>(e.out_code0 + px0 + c) = k0;
+    if (e.out_code1 && c < e.code1_cp)  // same01: two consumers with the same range, the same codes
       *reinterpret_cast<int*>(e.out_code1 + (((int64_t)n * e.code1_hp + ho + e.code1_pad) * e.code1_wp + wo + e.code1_pad) *
-                                                e.code1_cp + c) = pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
+                                                e.code1_cp + c) =
+          same01 ? k0 : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
   }
 }
 

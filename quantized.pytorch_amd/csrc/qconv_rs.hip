@@ -9,23 +9,20 @@ namespace rb {
 // ---------------------------------------------------------------- streamed resident band (rs)
 // qconv_rb_kernel's tile and main loop (one block per CU owns whole images x BM channels, the
 // band resident in LDS as 32-byte planes, each wave's weights straight into VGPRs), with the
-// block's serial phases taken off the K loop's critical path:
-// * the band arrives in CHUNKS of 2H planes (64H channels), in the order the K loop consumes
-//   them: the loop starts when chunk 0 has landed, and each wave issues its pieces of chunk c + 1
-//   during chunk c's first K steps, one per step, behind that step's weight refill (so the
-//   compiler's own weight waits -- vmcnt is in order -- have already covered a piece when its
-//   chunk begins; a raw s_barrier then publishes the chunk to the other waves);
+// block's serial phases taken off the critical path:
+// * the band arrives in CHUNKS of 2H planes (64H channels) in the order the K loop consumes
+//   them; the loop starts when chunk 0 has landed.  A wave's VMEM operations complete in order
+//   (one vmcnt), so every LDS-DMA a wave issues is implicitly waited for by its next weight wait
+//   after it: an in-loop DMA gets DA - 1 K steps to land, no more.  Hence the issue order at
+//   kernel start is chunk 0, the first DA - 1 weight steps, then (left in flight) chunk 1 and the
+//   epilogue data, and each later chunk c + 1 is issued at chunk c's boundary; a raw s_barrier at
+//   each boundary publishes the chunk to the other waves;
 // * sum_valid(q'_x): each thread sums its band pixels' channels chunk by chunk at the chunk
-//   boundaries (v_dot4 against 1s) and publishes them after the last one (one more barrier), so
-//   only the 9-tap box sum remains for the epilogue;
+//   boundaries (v_dot4 against 1s); after the last, the block's output pixels' 9-tap box sums are
+//   computed once (one LDS word per pixel) behind one more barrier, so the epilogue reads one
+//   word per pixel tile;
 // * each wave DMAs the epilogue data of ITS OWN channels (per-channel vectors, border table, the
-//   EK_LUT code table rows) during the last chunk's K steps and waits only for its own DMA: no
-//   workgroup barrier after the K loop, so the waves of a SIMD drift apart and one's epilogue runs
-//   beside the other's MFMAs;
-// * NP = 2 passes: a wave computes its pixel tiles in two halves (K loop, epilogue, K loop,
-//   epilogue), the second pass's first weights fetched before the first epilogue; with PRIO the
-//   first wave of each SIMD runs at s_setprio 1, so the pair staggers and each epilogue overlaps
-//   the partner's MFMAs (MI355X_MICROARCH: the matrix pipe and VALU issue are shared per SIMD).
+//   EK_LUT code-table rows) and waits only for its own DMA: no workgroup barrier after the K loop.
 // The DMAs are inline asm (global_load_lds with m0), invisible to the compiler's waitcnt pass:
 // it neither drains them before the band reads nor miscounts its weight waits (invisible older
 // VMEM ops only make a counted wait stricter).  Outputs are bitwise those of every other
@@ -34,13 +31,12 @@ namespace rb {
 __device__ unsigned long long qnn_rs_stamps[1 << 18];
 #endif
 
-template <class C, int EK, int H, int NP, int PRIO>
+template <class C, int EK, int H>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4))) void qconv_rs_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
   constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
   constexpr int CPL = 2 * H;  // planes per chunk
-  constexpr int NPT = 4;      // band pixels per thread (geometry: nbp <= NPT * NT)
-  constexpr int TN0 = NP == 1 ? TN : (TN + 1) / 2;
+  constexpr int NPT = 1;      // band pixels / output pixels per thread (geometry: nbp, npx <= NT)
   constexpr int CW = 16 * TM;  // this wave's channels
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
 
@@ -88,12 +84,13 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   const int nchunk = g.npl / CPL;
   const int npr = (g.ppp + W - 1) / W;  // this wave's ranges r = wave + W*k of each plane
   const int ppc = npr * CPL;             // its pieces of one chunk
-  auto issue_chunk = [&](int c, int i) { issue_piece(wave + W * (i / CPL), c * CPL + i % CPL); };
-  for (int i = 0; i < ppc; ++i) issue_chunk(0, i);
+  auto issue_chunk = [&](int c) {
+    for (int i = 0; i < ppc; ++i) issue_piece(wave + W * (i / CPL), c * CPL + i % CPL);
+  };
 
   // ---- the epilogue data of this wave's channels cw0 .. cw0 + CW (qconv_common.h stage_epi's
-  // layout), as jobs: per vector / table array one 4-byte-per-lane DMA per 64 channels, then the
-  // EK_LUT code-table rows (1 KiB = 4 rows per 16-byte-per-lane DMA)
+  // layout): per vector / table array one 4-byte-per-lane DMA per 64 channels, then the EK_LUT
+  // code-table rows (1 KiB = 4 rows per 16-byte-per-lane DMA)
   const bool lut_on = EK == EK_LUT && g.lut;
   int8_t* const epi = smem + p.epi_off;
   const int cw0 = wm * CW;
@@ -101,27 +98,16 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   constexpr int VJ = (CW + 63) / 64;  // DMAs per array
   const int nvec = (EK != EK_NCHW && e.bn_mean) ? 7 : 3;
   const int narr = nvec + e.nclass + (EK == EK_GEN ? 4 * e.nres : 0);
-  const int nvj = narr * VJ;
-  const int njobs = nvj + (lut_on ? CW / 4 : 0);
-  auto epi_job = [&](int k) {
-    if (k < nvj) {
-      const int v = k / VJ, kk = k - v * VJ;
+  const int njobs = narr * VJ + (lut_on ? CW / 4 : 0);  // this wave's epilogue DMAs
+  auto issue_epi = [&] {
+    for (int v = 0; v < narr; ++v) {
       const int arr = v < nvec ? v : 7 + (v - nvec);
-      const int cl = cw0 + 64 * kk + lane;  // local channel of this lane
-      int c = c0 + cl;
-      c = c < cmax ? c : cmax;
       const float* src;
+      bool zero = false;
       switch (arr) {
         case 0: src = e.sxsw; break;
         case 1: src = e.sxbw; break;
-        case 2:  // no bias: zeros from the input's 128-byte zero page
-          if (!e.bias) {
-            src = reinterpret_cast<const float*>(x + d.zero_off);
-            c = lane & 31;
-          } else {
-            src = e.bias;
-          }
-          break;
+        case 2: src = e.bias; zero = !e.bias; break;  // no bias: zeros from the input's zero page
         case 3: src = e.bn_mean; break;
         case 4: src = e.bn_sq; break;
         case 5: src = e.bn_wq; break;
@@ -136,31 +122,45 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
           }
           break;
       }
-      const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(epi + 4 * (arr * BM + cw0 + 64 * kk)));
-      if (CW % 64 == 0 || 64 * kk + lane < CW)  // lanes past this wave's channels write nothing
-        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(src + c) : "memory", "m0");
-    } else if (k < njobs) {
-      const int jl = k - nvj;  // rows cw0 + 4 jl .. + 3
-      int c = c0 + cw0 + 4 * jl + (lane >> 4);
-      c = c < cmax ? c : cmax;
-      const int8_t* src = e.lut + (int64_t)c * 256 + 16 * (lane & 15);
-      const uint32_t m =
-          __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(epi + 4 * (7 + e.nclass) * BM + 256 * (cw0 + 4 * jl)));
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+#pragma unroll
+      for (int kk = 0; kk < VJ; ++kk) {
+        int c = c0 + cw0 + 64 * kk + lane;
+        c = c < cmax ? c : cmax;
+        const float* sp = zero ? reinterpret_cast<const float*>(x + d.zero_off) + (lane & 31) : src + c;
+        const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(epi + 4 * (arr * BM + cw0 + 64 * kk)));
+        if (CW % 64 == 0 || 64 * kk + lane < CW)  // lanes past this wave's channels write nothing
+          asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(sp) : "memory", "m0");
+      }
+    }
+    if (lut_on) {
+      for (int jl = 0; jl < CW / 4; ++jl) {  // rows cw0 + 4 jl .. + 3
+        int c = c0 + cw0 + 4 * jl + (lane >> 4);
+        c = c < cmax ? c : cmax;
+        const int8_t* src = e.lut + (int64_t)c * 256 + 16 * (lane & 15);
+        const uint32_t m =
+            __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(epi + 4 * (7 + e.nclass) * BM + 256 * (cw0 + 4 * jl)));
+        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+      }
     }
   };
 
   // ---- the lane's band offset of output tile j (block pixel (wn*TN + j)*16 + (lane & 15); past
   // the block it stands in for the block's last pixel and is never stored)
   const int npx_blk = __builtin_amdgcn_readfirstlane((r0 + g.rows <= nrows_all ? g.rows : nrows_all - r0) * d.wo);
-  auto band_px = [&](int j) {
-    int q = (wn * TN + j) * 16 + (lane & 15);
+  auto band_px = [&](int q) {  // band pixel of tap (0, 0) of block pixel q
     q = q < npx_blk ? q : npx_blk - 1;
     const int rr = q / d.wo, col = q - rr * d.wo;
     const int r = r0 + rr, n = r / d.ho, ho = r - n * d.ho;
-    return (n * d.hp + ho * d.sh - R0) * g.wb + col;  // band pixel of tap (0, 0)
+    return (n * d.hp + ho * d.sh - R0) * g.wb + col;
   };
   const int lsel = (lane >> 5) * g.pl + 16 * ((lane >> 4) & 1);
+  int pb[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) pb[j] = band_px((wn * TN + j) * 16 + (lane & 15)) * 32 + lsel;
+
+  int* s_hc = reinterpret_cast<int*>(smem + g.cls_off);  // hcls[ho], then wcls[wo] (raw class ids)
+  int* s_ps = reinterpret_cast<int*>(smem + g.psum_off);  // band pixel channel sums
+  int* s_box = reinterpret_cast<int*>(smem + p.scr_off);  // the block's output pixels' box sums
 
   // ---- weights: rows c0 + cw0 + 16*i + (lane & 15), K bytes 16*(lane >> 4) of each step
   const int8_t* wblk = w + (int64_t)c0 * d.kpad;
@@ -192,25 +192,30 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
     for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const v4i*>(base + aoff[i]);
     if (H * cl.gp + cl.h < d.cp / 64 - 1 || cl.t < p.taps - 1 || cl.h < H - 1) advance(cl);  // clamp at the last step
   };
-  auto preload = [&] {
-    cl = {0, 0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
-  };
-  preload();
 
-  // LDS constants
-  int* s_tap = reinterpret_cast<int*>(smem + g.tap_off);
-  int* s_hc = reinterpret_cast<int*>(smem + g.cls_off);
-  int* s_ps = reinterpret_cast<int*>(smem + g.psum_off);
-  if (tid < p.taps) {
-    const int tr = tid / d.kw, tc = tid - tr * d.kw;
-    s_tap[tid] = tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc);
+  // issue order at start: the border classes and chunk 0, the first weights, chunk 1 (or the
+  // epilogue data); the class tables by 4-byte-per-lane DMA (wave 0), 64 entries per job
+  if (wave == 0) {
+    for (int i0 = 0; i0 < d.ho + d.wo; i0 += 64) {
+      const int i = i0 + lane;
+      const int* src = i < d.ho ? p.e.hcls + i : p.e.wcls + (i < d.ho + d.wo ? i - d.ho : d.wo - 1);
+      const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(s_hc + i0));
+      if (i < d.ho + d.wo)
+        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+    }
   }
-  for (int i = tid; i < d.ho + d.wo; i += NT) s_hc[i] = i < d.ho ? p.e.hcls[i] * p.e.nwc : p.e.wcls[i - d.ho];
+  issue_chunk(0);
+#pragma unroll
+  for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
+  if (nchunk > 1) issue_chunk(1);
+  // the epilogue data (L2-resident: it lands during chunk 0's wait, and the first in-loop weight
+  // wait covers it); issued here rather than in the loop, whose registers would have to carry
+  // every epilogue pointer through the K steps
+  issue_epi();
 
-  // channel sums of this thread's band pixels, accumulated chunk by chunk; published (one more
-  // barrier) once the last chunk is summed
+
+  // channel sums of this thread's band pixels, accumulated chunk by chunk; after the last chunk
+  // the output pixels' box sums (two barriers: all band sums written, all box sums read them)
   int psum[NPT];
 #pragma unroll
   for (int u = 0; u < NPT; ++u) psum[u] = 0;
@@ -242,113 +247,104 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
       for (int u = 0; u < NPT; ++u)
         if (tid + NT * u < g.nbp) s_ps[tid + NT * u] = psum[u];
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      int bx[NPT];
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int q = tid + NT * u;
+        bx[u] = 0;
+        if (q < npx_blk) {
+          const int b0 = band_px(q);
+          int tr = 0, tc = 0;
+          for (int tt = 0; tt < p.taps; ++tt) {
+            bx[u] += s_ps[b0 + tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc)];
+            if (++tc == d.kw) tc = 0, ++tr;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NPT; ++u)
+        if (tid + NT * u < npx_blk) s_box[tid + NT * u] = bx[u];
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
   };
 
-  // chunk 0 (this wave's pieces, then every wave's) and the LDS constants
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((DA - 1) * TM) : "memory");
+  // chunk 0 and the border classes (this wave's DMA: counted, chunk 1's pieces and the first
+  // weights behind them), then every wave's
+  // (chunk 1's pieces and the epilogue data stay in flight: the first in-loop weight wait
+  // covers them)
+  wait_vmcnt_rt((DA - 1) * TM + (nchunk > 1 ? CPL : 0) + njobs);
+  asm volatile("s_barrier" ::: "memory");
   sum_chunk(0);
-  if (PRIO && wave < W / 2) __builtin_amdgcn_s_setprio(1);
 #if QNN_STAMP
   RB_TS(ts1);
 #endif
 
-  const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
-  const int HoWo = d.ho * d.wo;
-  const int lm = r0 * d.wo + npx_blk - 1;  // the block's last pixel (stand-in of slots past it)
-  const int ln = lm / HoWo, lho = (lm - ln * HoWo) / d.wo, lwo = lm - ln * HoWo - lho * d.wo;
-
-  // ---- one pass: the K loop over tiles J0 .. J0 + TNP of this wave, then their epilogue
-  auto pass = [&](auto tnc, auto j0c) {
-    constexpr int TNP = decltype(tnc)::value, J0 = decltype(j0c)::value;
-    constexpr bool FIRST = J0 == 0, LAST = J0 + TNP == TN;
-    using CP = Cfg<C::WGM, C::WGN, TM, TNP, DA, 1>;
-    int pb[TNP];
+  v4i acc[TM][TN];
 #pragma unroll
-    for (int j = 0; j < TNP; ++j) pb[j] = band_px(J0 + j) * 32 + lsel;
-    v4i acc[TM][TNP];
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+  Cur cc = {0, 0, 0, 0, 0};
+  int chunk = 0;
+  auto step = [&](auto slotc) {
+    constexpr int SL = decltype(slotc)::value;
+    const int dt = cc.tr * g.wb + (g.s2 ? (cc.tc & 1) * g.we + (cc.tc >> 1) : cc.tc);
+    const int boff = (2 * (H * cc.gp + cc.h)) * g.pl + 32 * dt;
+    v4i fb[TN];
 #pragma unroll
-      for (int j = 0; j < TNP; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
-
-    Cur cc = {0, 0, 0, 0, 0};
-    int chunk = 0, bg = 0;  // (first pass) current chunk; background jobs issued in it
-    auto background = [&] {
-      if constexpr (FIRST) {
-        if (chunk + 1 < nchunk) {
-          if (bg < ppc) issue_chunk(chunk + 1, bg++);
-        } else {
-          if (bg < njobs) epi_job(bg++);
-          if (bg < njobs) epi_job(bg++);
-          if (bg < njobs) epi_job(bg++);
-        }
-      }
-    };
-    auto step = [&](auto slotc) {
-      constexpr int SL = decltype(slotc)::value;
-      const int dt = cc.tr * g.wb + (g.s2 ? (cc.tc & 1) * g.we + (cc.tc >> 1) : cc.tc);
-      const int boff = (2 * (H * cc.gp + cc.h)) * g.pl + 32 * dt;
-      v4i fb[TNP];
+    for (int j = 0; j < TN; ++j) {
+      v4i r;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(pb[j] + boff));
+      fb[j] = r;
+    }
+    static_for<TN>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      lds_wait<TN - 1 - j>();
 #pragma unroll
-      for (int j = 0; j < TNP; ++j) {
-        v4i r;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(pb[j] + boff));
-        fb[j] = r;
-      }
-      static_for<TNP>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        lds_wait<TNP - 1 - j>();
-#pragma unroll
-        for (int i = 0; i < TM; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[SL][i], fb[j], acc[i][j], 0, 0, 0);
-      });
-      __builtin_amdgcn_sched_barrier(0);
-      load_a(fa[(SL + DA - 1) % DA]);
-      background();
-      advance(cc);
-    };
+      for (int i = 0; i < TM; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[SL][i], fb[j], acc[i][j], 0, 0, 0);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    load_a(fa[(SL + DA - 1) % DA]);
+    advance(cc);
+  };
 #pragma nounroll
-    for (int k0 = 0; k0 < KS; k0 += DA) {
-      if constexpr (FIRST) {
-        if (k0 > 0 && k0 % SPC == 0) {  // chunk boundary: this wave's pieces landed (counted), then every wave's
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * TM) : "memory");
-          asm volatile("s_barrier" ::: "memory");
-          ++chunk;
-          bg = 0;
-          sum_chunk(chunk);
-        }
-      }
-      step(std::integral_constant<int, 0>{});
-      if constexpr (DA > 1) step(std::integral_constant<int, 1>{});
-      if constexpr (DA > 2) step(std::integral_constant<int, 2>{});
-      if constexpr (DA > 3) step(std::integral_constant<int, 3>{});
+  for (int k0 = 0; k0 < KS; k0 += DA) {
+    if (k0 > 0 && k0 % SPC == 0) {  // chunk boundary: this wave's pieces landed (counted), then every wave's
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * TM) : "memory");
+      asm volatile("s_barrier" ::: "memory");
+      ++chunk;
+      if (chunk + 1 < nchunk) issue_chunk(chunk + 1);
+      sum_chunk(chunk);
     }
+    step(std::integral_constant<int, 0>{});
+    if constexpr (DA > 1) step(std::integral_constant<int, 1>{});
+    if constexpr (DA > 2) step(std::integral_constant<int, 2>{});
+    if constexpr (DA > 3) step(std::integral_constant<int, 3>{});
+  }
 #if QNN_STAMP
-    if (FIRST) RB_TS(ts2);
-    else RB_TS(ts6);
+  RB_TS(ts2);
 #endif
-    if constexpr (FIRST) {
-      while (bg < njobs) epi_job(bg++);  // (a last chunk shorter than the jobs)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's epilogue data, the clamped tail weights
-    }
-    if constexpr (!LAST) preload();  // the next pass's first weights, ahead of this epilogue's stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's epilogue data, the clamped tail weights
 #if QNN_STAMP
-    if (FIRST) RB_TS(ts3);
+  RB_TS(ts3);
 #endif
-    int sumq[TNP];
+  int sumq[TN];
 #pragma unroll
-    for (int j = 0; j < TNP; ++j) {
-      sumq[j] = 0;
-      const int b0 = (pb[j] - lsel) >> 5;
-      int tr = 0, tc = 0;
-      for (int tt = 0; tt < p.taps; ++tt) {
-        sumq[j] += s_ps[b0 + tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc)];
-        if (++tc == d.kw) tc = 0, ++tr;
-      }
-    }
-    int cq = (wn * TN + J0) * 16 + (lane & 15);
+  for (int j = 0; j < TN; ++j) {
+    int q = (wn * TN + j) * 16 + (lane & 15);
+    q = q < npx_blk ? q : npx_blk - 1;
+    sumq[j] = s_box[q];
+  }
+#if QNN_STAMP
+  RB_TS(ts5);
+#endif
+  {
+    const int HoWo = d.ho * d.wo;
+    int cq = (wn * TN) * 16 + (lane & 15);
     int cm = r0 * d.wo + (cq < npx_blk ? cq : npx_blk - 1);
     int cn = cm / HoWo, cho = (cm - cn * HoWo) / d.wo, cwo = cm - cn * HoWo - cho * d.wo;
+    const int lm = r0 * d.wo + npx_blk - 1;
+    const int ln = lm / HoWo, lho = (lm - ln * HoWo) / d.wo, lwo = lm - ln * HoWo - lho * d.wo;
     auto pixel = [&](int j, q16::Pix& P, int& pc) {
       if (j > 0) {
         cq += 16;
@@ -363,11 +359,12 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
       P.n = P.ok ? cn : ln;
       P.ho = P.ok ? cho : lho;
       P.wo = P.ok ? cwo : lwo;
-      pc = s_hc[P.ho] + s_hc[d.ho + P.wo];
+      pc = s_hc[P.ho] * e.nwc + s_hc[d.ho + P.wo];
     };
     if (EK == EK_LUT && g.lut && c0 + BM <= d.cout && c0 + BM <= e.code0_cp) {
       const float* s_f = reinterpret_cast<const float*>(epi);
       const int8_t* s_lut = epi + 4 * (7 + e.nclass) * BM;
+      const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
       const int gq = lane >> 4;
       float4 sw[TM], bw[TM], bi[TM];
 #pragma unroll
@@ -378,7 +375,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
         bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl_);
       }
 #pragma unroll
-      for (int j = 0; j < TNP; ++j) {
+      for (int j = 0; j < TN; ++j) {
         q16::Pix P;
         int pc;
         pixel(j, P, pc);
@@ -406,23 +403,17 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
         }
       }
     } else {
-      q16::epilogue_rb<CP, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
+      q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
     }
+  }
 #if QNN_STAMP
-    if (FIRST) RB_TS(ts5);
-#endif
-  };
-  pass(std::integral_constant<int, TN0>{}, std::integral_constant<int, 0>{});
-  if constexpr (NP > 1) pass(std::integral_constant<int, TN - TN0>{}, std::integral_constant<int, TN0>{});
-#if QNN_STAMP
+  RB_TS(ts6);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   RB_TS(ts4);
-  if (NP == 1) ts6 = ts4;
   const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0 && blockIdx.x < (1 << 18) / (8 * W)) {
     unsigned long long* o = qnn_rs_stamps + ((size_t)blockIdx.x * W + wave) * 8;
-    // prologue (chunk 0), pass-0 K loop, its epilogue-data wait, pass-0 epilogue (box sums
-    // included), pass-1 K loop, pass-1 epilogue + store drain
+    // prologue (chunk 0), K loop, epilogue-data wait, box-sum reads, epilogue, store drain
     o[0] = rt0; o[1] = rt1; o[2] = ts1 - ts0; o[3] = ts2 - ts1; o[4] = ts3 - ts2; o[5] = ts5 - ts3;
     o[6] = ts6 - ts5; o[7] = ts4 - ts6;
   }
@@ -437,21 +428,22 @@ static int rs_plan(const Params& p, Params& q, Geo& g) {
   const int main = geometry(p, C::BM, C::BN, C::W, 1, 0, g);
   if (main < 0) return -1;
   const int cpl = 2 * H, spc = H * p.taps;
-  const int ppc = (int)cdiv(g.ppp, C::W) * cpl;
-  if (g.npl % cpl || spc % C::DA || ppc + C::DA - 1 > spc || g.nbp > 4 * C::NT)
-    return -1;
+  // one DMA range per wave and plane (the chunk-0 wait counts pieces at compile time); chunk
+  // boundaries on whole DA-step groups; one band pixel and one output pixel per thread
+  if (g.npl % cpl || spc % C::DA || g.ppp > C::W || g.nbp > C::NT || g.npx > C::NT) return -1;
   q = p;
+  const int box = (4 * g.npx + 15) & ~15;
   int epi = epi_bytes(p, C::BM);
   g.lut = 0;
-  if (EK == EK_LUT && main + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
-  if (main + epi > LDS_MAX) return -1;
-  q.epi_early = 1, q.epi_off = main, q.scr_off = 0;
-  return main + epi;
+  if (EK == EK_LUT && main + box + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
+  if (main + box + epi > LDS_MAX) return -1;
+  q.epi_early = 1, q.scr_off = main, q.epi_off = main + box;
+  return main + box + epi;
 }
 
-template <class C, int EK, int H, int NP, int PRIO>
+template <class C, int EK, int H>
 static int rs_launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  auto kern = qconv_rs_kernel<C, EK, H, NP, PRIO>;
+  auto kern = qconv_rs_kernel<C, EK, H>;
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -471,54 +463,39 @@ static int rs_launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStr
   return QNN_OK;
 }
 
-// the general chain spills beside more than 16 accumulator tiles (per pass): not built
-template <class C, int NP>
-constexpr bool rs_gen_ok() { return C::TM * ((C::TN + NP - 1) / NP) <= 16; }
-
-template <class C, int H, int NP, int PRIO>
+template <class C, int H>
 static int rs_launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   if (p.d.cp == 64 && H != 1) return arg_error("tile configuration not built for this layer / epilogue kind");
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return rs_launch_k<C, EK_NCHW, H, NP, PRIO>(x, w, p, s, occ);
-    case EK_LUT: return rs_launch_k<C, EK_LUT, H, NP, PRIO>(x, w, p, s, occ);
-    case EK_BNCODE: return rs_launch_k<C, EK_BNCODE, H, NP, PRIO>(x, w, p, s, occ);
-    default:
-      if constexpr (!rs_gen_ok<C, NP>()) return arg_error("tile configuration not built for this layer / epilogue kind");
-      else return rs_launch_k<C, EK_GEN, H, NP, PRIO>(x, w, p, s, occ);
+    case EK_NCHW: return rs_launch_k<C, EK_NCHW, H>(x, w, p, s, occ);
+    case EK_LUT: return rs_launch_k<C, EK_LUT, H>(x, w, p, s, occ);
+    case EK_BNCODE: return rs_launch_k<C, EK_BNCODE, H>(x, w, p, s, occ);
+    default:  // the general chain spills beside more than 16 accumulator tiles: not built
+      if constexpr (C::TM * C::TN > 16) return arg_error("tile configuration not built for this layer / epilogue kind");
+      else return rs_launch_k<C, EK_GEN, H>(x, w, p, s, occ);
   }
 }
 
-//   id  block (cout x px cols)  waves (each)    K order / passes
-//   0   256 x 208               8 (32 x 208)    H = 2, 1 pass           14x14 images (ResNet-50 layer 3, b256)
-//   1   256 x 208               8 (32 x 208)    H = 1, 1 pass
-//   2   256 x 208               8 (32 x 208)    H = 2, 2 passes, priority stagger
-//   3   256 x 208               8 (32 x 208)    H = 1, 2 passes, priority stagger
-//   4   256 x 208               8 (32 x 208)    H = 2, 2 passes
-//   5   256 x 224               8 (64 x 112)    H = 2, 2 passes, priority stagger
-//   6   256 x 112               8 (32 x 112)    H = 2, 2 passes, priority stagger   half 14x14 images (ResNet-18 layer 3, b128)
-//   7   256 x 112               8 (32 x 112)    H = 1, 1 pass
+//   id  block (cout x px cols)  waves (each)    weights in flight
+//   0   256 x 208               8 (32 x 208)    DA = 3      14x14 images (ResNet-50 layer 3, b256)
+//   1   256 x 208               8 (32 x 208)    DA = 4
+//   2   256 x 224               8 (64 x 112)    DA = 3      each band fragment feeds 4 MFMAs
+//   3   256 x 112               8 (32 x 112)    DA = 3      half 14x14 images (ResNet-18 layer 3, b128)
+//   4   256 x 112               8 (32 x 112)    DA = 4
+//   5   128 x 112               8 (16 x 112)    DA = 4      2 images of 7x7 on 512 channels (layer 4, b128)
 using S0 = Cfg<8, 1, 2, 13, 3, 1>;
+using S1 = Cfg<8, 1, 2, 13, 4, 1>;
 using S2 = Cfg<4, 2, 4, 7, 3, 1>;
-using S4 = Cfg<8, 1, 2, 7, 3, 1>;
-constexpr int NS = 8;
+using S3 = Cfg<8, 1, 2, 7, 3, 1>;
+using S4 = Cfg<8, 1, 2, 7, 4, 1>;
+using S5 = Cfg<8, 1, 1, 7, 4, 1>;
+constexpr int NS = 6;
 static const Info SINFO[NS] = {
-    {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f},
-    {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f}, {256, 112, 8, 1, 14, 1.10f}, {256, 112, 8, 1, 14, 1.10f},
+    {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f},
+    {256, 112, 8, 1, 14, 1.10f}, {256, 112, 8, 1, 14, 1.10f}, {128, 112, 8, 1, 7, 0.80f},
 };
 
-template <int K, class F>
-static auto rs_dispatch(F&& f) {
-  if constexpr (K == 0) return f(S0{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-  else if constexpr (K == 1) return f(S0{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-  else if constexpr (K == 2) return f(S0{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-  else if constexpr (K == 3) return f(S0{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-  else if constexpr (K == 4) return f(S0{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{});
-  else if constexpr (K == 5) return f(S2{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-  else if constexpr (K == 6) return f(S4{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-  else return f(S4{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-}
-
-template <class C, int H, int NP>
+template <class C, int H>
 static bool rs_ok_h(const Params& p) {
   if (p.d.cp == 64 && H != 1) return false;
   Params q;
@@ -527,20 +504,16 @@ static bool rs_ok_h(const Params& p) {
     case EK_NCHW: return rs_plan<C, EK_NCHW, H>(p, q, g) >= 0;
     case EK_LUT: return rs_plan<C, EK_LUT, H>(p, q, g) >= 0;
     case EK_BNCODE: return rs_plan<C, EK_BNCODE, H>(p, q, g) >= 0;
-    default: return rs_gen_ok<C, NP>() && rs_plan<C, EK_GEN, H>(p, q, g) >= 0;
+    default: return C::TM * C::TN <= 16 && rs_plan<C, EK_GEN, H>(p, q, g) >= 0;
   }
 }
 
-template <int K>
-static bool rs_ok_k(const Params& p) {
-  return rs_dispatch<K>([&](auto c, auto h, auto np, auto) { return rs_ok_h<decltype(c), h.value, np.value>(p); });
-}
-
-template <int K>
-static int rs_launch_kk(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  return rs_dispatch<K>([&](auto c, auto h, auto np, auto pr) {
-    return rs_launch_ek<decltype(c), h.value, np.value, pr.value>(x, w, p, s, occ);
-  });
+// 128-channel chunks (H = 2) where the channels allow, else 64 (cp = 64)
+template <class C>
+static bool rs_ok_c(const Params& p) { return p.d.cp == 64 ? rs_ok_h<C, 1>(p) : rs_ok_h<C, 2>(p); }
+template <class C>
+static int rs_launch_c(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  return p.d.cp == 64 ? rs_launch_ek<C, 1>(x, w, p, s, occ) : rs_launch_ek<C, 2>(x, w, p, s, occ);
 }
 
 }  // namespace rb
@@ -555,14 +528,12 @@ void rs_tile(int k, int* bm, int* bn) {
 bool rs_ok(int k, const Params& p) {
   using namespace rb;
   switch (k) {
-    case 0: return rs_ok_k<0>(p);
-    case 1: return rs_ok_k<1>(p);
-    case 2: return rs_ok_k<2>(p);
-    case 3: return rs_ok_k<3>(p);
-    case 4: return rs_ok_k<4>(p);
-    case 5: return rs_ok_k<5>(p);
-    case 6: return rs_ok_k<6>(p);
-    case 7: return rs_ok_k<7>(p);
+    case 0: return rs_ok_c<S0>(p);
+    case 1: return rs_ok_c<S1>(p);
+    case 2: return rs_ok_c<S2>(p);
+    case 3: return rs_ok_c<S3>(p);
+    case 4: return rs_ok_c<S4>(p);
+    case 5: return rs_ok_c<S5>(p);
     default: return false;
   }
 }
@@ -585,14 +556,12 @@ double rs_cost(int k, const Params& p) {
 int rs_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   using namespace rb;
   switch (k) {
-    case 0: return rs_launch_kk<0>(x, w, p, s, occ);
-    case 1: return rs_launch_kk<1>(x, w, p, s, occ);
-    case 2: return rs_launch_kk<2>(x, w, p, s, occ);
-    case 3: return rs_launch_kk<3>(x, w, p, s, occ);
-    case 4: return rs_launch_kk<4>(x, w, p, s, occ);
-    case 5: return rs_launch_kk<5>(x, w, p, s, occ);
-    case 6: return rs_launch_kk<6>(x, w, p, s, occ);
-    default: return rs_launch_kk<7>(x, w, p, s, occ);
+    case 0: return rs_launch_c<S0>(x, w, p, s, occ);
+    case 1: return rs_launch_c<S1>(x, w, p, s, occ);
+    case 2: return rs_launch_c<S2>(x, w, p, s, occ);
+    case 3: return rs_launch_c<S3>(x, w, p, s, occ);
+    case 4: return rs_launch_c<S4>(x, w, p, s, occ);
+    default: return rs_launch_c<S5>(x, w, p, s, occ);
   }
 }
 

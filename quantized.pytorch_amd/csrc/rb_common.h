@@ -44,6 +44,14 @@ __device__ __forceinline__ void lds_wait() {
 
 // WGM x WGN waves; a wave owns TM 16-channel tiles x TN 16-pixel tiles; DA weight register
 // slots per wave (DA - 1 K steps in flight); BPC blocks per CU the registers and LDS must allow.
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the counter's 63: a longer wait)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  n = n < 63 ? n : 63;
+  static_for<64>([&](auto c) {
+    if (n == decltype(c)::value) wait_vmcnt<decltype(c)::value>();
+  });
+}
+
 template <int WGM_, int WGN_, int TM_, int TN_, int DA_, int BPC_>
 struct Cfg {
   static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, DA = DA_, BPC = BPC_;
