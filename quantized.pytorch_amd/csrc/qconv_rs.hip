@@ -31,7 +31,9 @@ namespace rb {
 __device__ unsigned long long qnn_rs_stamps[1 << 18];
 #endif
 
-template <class C, int EK, int H>
+// LATE: chunk 1 and the epilogue data issued after chunk 0's barrier instead of at kernel start
+// (their issue then stays out of chunk 0's wait; the first in-loop weight wait covers them)
+template <class C, int EK, int H, int LATE>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4))) void qconv_rs_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
   constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
@@ -207,11 +209,12 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   issue_chunk(0);
 #pragma unroll
   for (int s = 0; s < DA - 1; ++s) load_a(fa[s]);
-  if (nchunk > 1) issue_chunk(1);
-  // the epilogue data (L2-resident: it lands during chunk 0's wait, and the first in-loop weight
-  // wait covers it); issued here rather than in the loop, whose registers would have to carry
-  // every epilogue pointer through the K steps
-  issue_epi();
+  // chunk 1 and the epilogue data (L2-resident); issued before the loop, whose registers would
+  // otherwise carry every epilogue pointer through the K steps
+  if (!LATE) {
+    if (nchunk > 1) issue_chunk(1);
+    issue_epi();
+  }
 
 
   // channel sums of this thread's band pixels, accumulated chunk by chunk; after the last chunk
@@ -272,8 +275,13 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   // weights behind them), then every wave's
   // (chunk 1's pieces and the epilogue data stay in flight: the first in-loop weight wait
   // covers them)
-  wait_vmcnt_rt((DA - 1) * TM + (nchunk > 1 ? CPL : 0) + njobs);
+  if (LATE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * TM) : "memory");
+  else wait_vmcnt_rt((DA - 1) * TM + (nchunk > 1 ? CPL : 0) + njobs);
   asm volatile("s_barrier" ::: "memory");
+  if (LATE) {
+    if (nchunk > 1) issue_chunk(1);
+    issue_epi();
+  }
   sum_chunk(0);
 #if QNN_STAMP
   RB_TS(ts1);
@@ -441,9 +449,9 @@ static int rs_plan(const Params& p, Params& q, Geo& g) {
   return main + box + epi;
 }
 
-template <class C, int EK, int H>
+template <class C, int EK, int H, int LATE>
 static int rs_launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  auto kern = qconv_rs_kernel<C, EK, H>;
+  auto kern = qconv_rs_kernel<C, EK, H, LATE>;
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
   if (attr != hipSuccess) return hip_check(attr, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -463,41 +471,21 @@ static int rs_launch_k(const int8_t* x, const int8_t* w, const Params& p, hipStr
   return QNN_OK;
 }
 
-template <class C, int H>
+template <class C, int H, int LATE>
 static int rs_launch_ek(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  if (p.d.cp == 64 && H != 1) return arg_error("tile configuration not built for this layer / epilogue kind");
   switch (epi_kind(p.e)) {
-    case EK_NCHW: return rs_launch_k<C, EK_NCHW, H>(x, w, p, s, occ);
-    case EK_LUT: return rs_launch_k<C, EK_LUT, H>(x, w, p, s, occ);
-    case EK_BNCODE: return rs_launch_k<C, EK_BNCODE, H>(x, w, p, s, occ);
+    case EK_NCHW: return rs_launch_k<C, EK_NCHW, H, LATE>(x, w, p, s, occ);
+    case EK_LUT: return rs_launch_k<C, EK_LUT, H, LATE>(x, w, p, s, occ);
+    case EK_BNCODE: return rs_launch_k<C, EK_BNCODE, H, LATE>(x, w, p, s, occ);
     default:  // the general chain spills beside more than 16 accumulator tiles: not built
       if constexpr (C::TM * C::TN > 16) return arg_error("tile configuration not built for this layer / epilogue kind");
-      else return rs_launch_k<C, EK_GEN, H>(x, w, p, s, occ);
+      else return rs_launch_k<C, EK_GEN, H, LATE>(x, w, p, s, occ);
   }
 }
 
-//   id  block (cout x px cols)  waves (each)    weights in flight
-//   0   256 x 208               8 (32 x 208)    DA = 3      14x14 images (ResNet-50 layer 3, b256)
-//   1   256 x 208               8 (32 x 208)    DA = 4
-//   2   256 x 224               8 (64 x 112)    DA = 3      each band fragment feeds 4 MFMAs
-//   3   256 x 112               8 (32 x 112)    DA = 3      half 14x14 images (ResNet-18 layer 3, b128)
-//   4   256 x 112               8 (32 x 112)    DA = 4
-//   5   128 x 112               8 (16 x 112)    DA = 4      2 images of 7x7 on 512 channels (layer 4, b128)
-using S0 = Cfg<8, 1, 2, 13, 3, 1>;
-using S1 = Cfg<8, 1, 2, 13, 4, 1>;
-using S2 = Cfg<4, 2, 4, 7, 3, 1>;
-using S3 = Cfg<8, 1, 2, 7, 3, 1>;
-using S4 = Cfg<8, 1, 2, 7, 4, 1>;
-using S5 = Cfg<8, 1, 1, 7, 4, 1>;
-constexpr int NS = 6;
-static const Info SINFO[NS] = {
-    {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f},
-    {256, 112, 8, 1, 14, 1.10f}, {256, 112, 8, 1, 14, 1.10f}, {128, 112, 8, 1, 7, 0.80f},
-};
-
 template <class C, int H>
 static bool rs_ok_h(const Params& p) {
-  if (p.d.cp == 64 && H != 1) return false;
+  if (p.d.cp < 128 * H) return false;  // (a 64-channel layer has one chunk of H = 1)
   Params q;
   Geo g;
   switch (epi_kind(p.e)) {
@@ -508,12 +496,52 @@ static bool rs_ok_h(const Params& p) {
   }
 }
 
-// 128-channel chunks (H = 2) where the channels allow, else 64 (cp = 64)
-template <class C>
-static bool rs_ok_c(const Params& p) { return p.d.cp == 64 ? rs_ok_h<C, 1>(p) : rs_ok_h<C, 2>(p); }
-template <class C>
-static int rs_launch_c(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
-  return p.d.cp == 64 ? rs_launch_ek<C, 1>(x, w, p, s, occ) : rs_launch_ek<C, 2>(x, w, p, s, occ);
+//   id  block (cout x px cols)  waves (each)    K chunks   chunk 1 + epilogue data
+//   0   256 x 208               8 (32 x 208)    128 ch     at start        14x14 images (ResNet-50 layer 3, b256)
+//   1   256 x 208               8 (32 x 208)    64 ch      at start
+//   2   256 x 208               8 (32 x 208)    128 ch     after chunk 0
+//   3   256 x 208               8 (32 x 208)    64 ch      after chunk 0
+//   4   256 x 224               8 (64 x 112)    128 ch     at start        each band fragment feeds 4 MFMAs
+//   5   256 x 112               8 (32 x 112)    128 ch     at start        half 14x14 images (ResNet-18 layer 3, b128)
+//   6   256 x 112               8 (32 x 112)    64 ch      after chunk 0
+//   7   128 x 112               8 (16 x 112)    128 ch     at start        2 images of 7x7 on 512 channels (layer 4, b128)
+using S0 = Cfg<8, 1, 2, 13, 3, 1>;
+using S2 = Cfg<4, 2, 4, 7, 3, 1>;
+using S3 = Cfg<8, 1, 2, 7, 3, 1>;
+using S5 = Cfg<8, 1, 1, 7, 4, 1>;
+constexpr int NS = 8;
+static const Info SINFO[NS] = {
+    {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f},
+    {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f}, {256, 112, 8, 1, 14, 1.10f},
+    {256, 112, 8, 1, 14, 1.10f}, {128, 112, 8, 1, 7, 0.80f},
+};
+
+template <int K, class F>
+static auto rs_cfg(F&& f) {
+  using I2 = std::integral_constant<int, 2>;
+  using I1 = std::integral_constant<int, 1>;
+  using I0 = std::integral_constant<int, 0>;
+  if constexpr (K == 0) return f(S0{}, I2{}, I0{});
+  else if constexpr (K == 1) return f(S0{}, I1{}, I0{});
+  else if constexpr (K == 2) return f(S0{}, I2{}, I1{});
+  else if constexpr (K == 3) return f(S0{}, I1{}, I1{});
+  else if constexpr (K == 4) return f(S2{}, I2{}, I0{});
+  else if constexpr (K == 5) return f(S3{}, I2{}, I0{});
+  else if constexpr (K == 6) return f(S3{}, I1{}, I1{});
+  else return f(S5{}, I2{}, I0{});
+}
+
+template <int K>
+static bool rs_ok_k(const Params& p) {
+  return rs_cfg<K>([&](auto c, auto h, auto) { return rs_ok_h<decltype(c), decltype(h)::value>(p); });
+}
+template <int K>
+static int rs_launch_kk(const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
+  return rs_cfg<K>([&](auto c, auto h, auto late) {
+    if (!rs_ok_h<decltype(c), decltype(h)::value>(p))
+      return arg_error("tile configuration not built for this layer / epilogue kind");
+    return rs_launch_ek<decltype(c), decltype(h)::value, decltype(late)::value>(x, w, p, s, occ);
+  });
 }
 
 }  // namespace rb
@@ -528,12 +556,14 @@ void rs_tile(int k, int* bm, int* bn) {
 bool rs_ok(int k, const Params& p) {
   using namespace rb;
   switch (k) {
-    case 0: return rs_ok_c<S0>(p);
-    case 1: return rs_ok_c<S1>(p);
-    case 2: return rs_ok_c<S2>(p);
-    case 3: return rs_ok_c<S3>(p);
-    case 4: return rs_ok_c<S4>(p);
-    case 5: return rs_ok_c<S5>(p);
+    case 0: return rs_ok_k<0>(p);
+    case 1: return rs_ok_k<1>(p);
+    case 2: return rs_ok_k<2>(p);
+    case 3: return rs_ok_k<3>(p);
+    case 4: return rs_ok_k<4>(p);
+    case 5: return rs_ok_k<5>(p);
+    case 6: return rs_ok_k<6>(p);
+    case 7: return rs_ok_k<7>(p);
     default: return false;
   }
 }
@@ -556,12 +586,14 @@ double rs_cost(int k, const Params& p) {
 int rs_launch(int k, const int8_t* x, const int8_t* w, const Params& p, hipStream_t s, Occ* occ) {
   using namespace rb;
   switch (k) {
-    case 0: return rs_launch_c<S0>(x, w, p, s, occ);
-    case 1: return rs_launch_c<S1>(x, w, p, s, occ);
-    case 2: return rs_launch_c<S2>(x, w, p, s, occ);
-    case 3: return rs_launch_c<S3>(x, w, p, s, occ);
-    case 4: return rs_launch_c<S4>(x, w, p, s, occ);
-    default: return rs_launch_c<S5>(x, w, p, s, occ);
+    case 0: return rs_launch_kk<0>(x, w, p, s, occ);
+    case 1: return rs_launch_kk<1>(x, w, p, s, occ);
+    case 2: return rs_launch_kk<2>(x, w, p, s, occ);
+    case 3: return rs_launch_kk<3>(x, w, p, s, occ);
+    case 4: return rs_launch_kk<4>(x, w, p, s, occ);
+    case 5: return rs_launch_kk<5>(x, w, p, s, occ);
+    case 6: return rs_launch_kk<6>(x, w, p, s, occ);
+    default: return rs_launch_kk<7>(x, w, p, s, occ);
   }
 }
 
