@@ -162,7 +162,8 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
 
   int* s_hc = reinterpret_cast<int*>(smem + g.cls_off);  // hcls[ho], then wcls[wo] (raw class ids)
   int* s_ps = reinterpret_cast<int*>(smem + g.psum_off);  // band pixel channel sums
-  int* s_box = reinterpret_cast<int*>(smem + p.scr_off);  // the block's output pixels' box sums
+  // the block's output pixels: {box sum of q', border class, flattened pixel m, n << 16 | ho << 8 | wo}
+  int4* s_px = reinterpret_cast<int4*>(smem + p.scr_off);
 
   // ---- weights: rows c0 + cw0 + 16*i + (lane & 15), K bytes 16*(lane >> 4) of each step
   const int8_t* wblk = w + (int64_t)c0 * d.kpad;
@@ -215,6 +216,10 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
     if (nchunk > 1) issue_chunk(1);
     issue_epi();
   }
+#if QNN_STAMP
+  unsigned long long ta = 0, tb = 0, tc = 0;
+  RB_TS(ta);
+#endif
 
 
   // channel sums of this thread's band pixels, accumulated chunk by chunk; after the last chunk
@@ -250,23 +255,23 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
       for (int u = 0; u < NPT; ++u)
         if (tid + NT * u < g.nbp) s_ps[tid + NT * u] = psum[u];
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      int bx[NPT];
+      // each output pixel of the block, once: its receptive-field sum, border class and coordinates
+      // (the epilogue then reads one 16-byte word per pixel tile: no divisions, no loops)
 #pragma unroll
       for (int u = 0; u < NPT; ++u) {
         const int q = tid + NT * u;
-        bx[u] = 0;
         if (q < npx_blk) {
           const int b0 = band_px(q);
-          int tr = 0, tc = 0;
+          int bx = 0, tr = 0, tc = 0;
           for (int tt = 0; tt < p.taps; ++tt) {
-            bx[u] += s_ps[b0 + tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc)];
+            bx += s_ps[b0 + tr * g.wb + (g.s2 ? (tc & 1) * g.we + (tc >> 1) : tc)];
             if (++tc == d.kw) tc = 0, ++tr;
           }
+          const int m = r0 * d.wo + q, HoWo = d.ho * d.wo;
+          const int n = m / HoWo, ho = (m - n * HoWo) / d.wo, wo = m - n * HoWo - ho * d.wo;
+          s_px[q] = make_int4(bx, s_hc[ho] * e.nwc + s_hc[d.ho + wo], m, (n << 16) | (ho << 8) | wo);
         }
       }
-#pragma unroll
-      for (int u = 0; u < NPT; ++u)
-        if (tid + NT * u < npx_blk) s_box[tid + NT * u] = bx[u];
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
   };
@@ -277,7 +282,13 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   // covers them)
   if (LATE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * TM) : "memory");
   else wait_vmcnt_rt((DA - 1) * TM + (nchunk > 1 ? CPL : 0) + njobs);
+#if QNN_STAMP
+  RB_TS(tb);
+#endif
   asm volatile("s_barrier" ::: "memory");
+#if QNN_STAMP
+  RB_TS(tc);
+#endif
   if (LATE) {
     if (nchunk > 1) issue_chunk(1);
     issue_epi();
@@ -341,33 +352,23 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   for (int j = 0; j < TN; ++j) {
     int q = (wn * TN + j) * 16 + (lane & 15);
     q = q < npx_blk ? q : npx_blk - 1;
-    sumq[j] = s_box[q];
+    sumq[j] = s_px[q].x;
   }
 #if QNN_STAMP
   RB_TS(ts5);
 #endif
   {
-    const int HoWo = d.ho * d.wo;
-    int cq = (wn * TN) * 16 + (lane & 15);
-    int cm = r0 * d.wo + (cq < npx_blk ? cq : npx_blk - 1);
-    int cn = cm / HoWo, cho = (cm - cn * HoWo) / d.wo, cwo = cm - cn * HoWo - cho * d.wo;
-    const int lm = r0 * d.wo + npx_blk - 1;
-    const int ln = lm / HoWo, lho = (lm - ln * HoWo) / d.wo, lwo = lm - ln * HoWo - lho * d.wo;
+    // this lane's pixel of tile j from the block's pixel table (a slot past the block stands in
+    // for the block's last pixel and is never stored)
     auto pixel = [&](int j, q16::Pix& P, int& pc) {
-      if (j > 0) {
-        cq += 16;
-        cwo += 16;
-        while (cwo >= d.wo) {
-          cwo -= d.wo;
-          if (++cho == d.ho) cho = 0, ++cn;
-        }
-      }
-      P.ok = cq < npx_blk;
-      P.m = P.ok ? r0 * d.wo + cq : lm;
-      P.n = P.ok ? cn : ln;
-      P.ho = P.ok ? cho : lho;
-      P.wo = P.ok ? cwo : lwo;
-      pc = s_hc[P.ho] * e.nwc + s_hc[d.ho + P.wo];
+      const int q = (wn * TN + j) * 16 + (lane & 15);
+      P.ok = q < npx_blk;
+      const int4 px = s_px[P.ok ? q : npx_blk - 1];
+      pc = px.y;
+      P.m = px.z;
+      P.n = (int)((unsigned)px.w >> 16);
+      P.ho = (px.w >> 8) & 255;
+      P.wo = px.w & 255;
     };
     if (EK == EK_LUT && g.lut && c0 + BM <= d.cout && c0 + BM <= e.code0_cp) {
       const float* s_f = reinterpret_cast<const float*>(epi);
@@ -421,9 +422,10 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0 && blockIdx.x < (1 << 18) / (8 * W)) {
     unsigned long long* o = qnn_rs_stamps + ((size_t)blockIdx.x * W + wave) * 8;
-    // prologue (chunk 0), K loop, epilogue-data wait, box-sum reads, epilogue, store drain
-    o[0] = rt0; o[1] = rt1; o[2] = ts1 - ts0; o[3] = ts2 - ts1; o[4] = ts3 - ts2; o[5] = ts5 - ts3;
-    o[6] = ts6 - ts5; o[7] = ts4 - ts6;
+    // issue (DMA + first weights), chunk-0 wait, its barrier, K loop (chunk-0 sums included),
+    // epilogue (epilogue-data wait and box sums included), store drain
+    o[0] = rt0; o[1] = rt1; o[2] = ta - ts0; o[3] = tb - ta; o[4] = tc - tb; o[5] = ts2 - tc;
+    o[6] = ts6 - ts2; o[7] = ts4 - ts6;
   }
 #endif
 }
@@ -439,8 +441,9 @@ static int rs_plan(const Params& p, Params& q, Geo& g) {
   // one DMA range per wave and plane (the chunk-0 wait counts pieces at compile time); chunk
   // boundaries on whole DA-step groups; one band pixel and one output pixel per thread
   if (g.npl % cpl || spc % C::DA || g.ppp > C::W || g.nbp > C::NT || g.npx > C::NT) return -1;
+  if (p.d.ho > 255 || p.d.wo > 255 || p.d.n > 65535) return -1;  // (the pixel table's packed coordinates)
   q = p;
-  const int box = (4 * g.npx + 15) & ~15;
+  const int box = 16 * g.npx;  // the pixel table (int4 per output pixel)
   int epi = epi_bytes(p, C::BM);
   g.lut = 0;
   if (EK == EK_LUT && main + box + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;

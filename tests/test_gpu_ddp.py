@@ -263,8 +263,7 @@ def _c5_worker(rank, world, port, out):
             assert logits is None
         del runner, eng
         torch.cuda.empty_cache()
-    if rank == 0:
-        res["state"] = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    res["state"] = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     torch.save(res, f"{out}.{rank}")
     dist.barrier()
     dist.destroy_process_group()
@@ -284,25 +283,16 @@ def test_sharded_engine_world2_c5_resnet50(gpu, tmp_path):
     got = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
     assert [got[r][512]["shard"] for r in range(2)] == [(0, 256), (256, 512)]
     assert [got[r][511]["shard"] for r in range(2)] == [(0, 256), (256, 511)]
-    # the merged calibration: rebuild each rank's own calibration here and merge it the same way
-    w = [b[0].shape[0] for b in (_c5_calib_batches(0, 2), _c5_calib_batches(1, 2))]
-    states = []
-    for r in range(2):
-        model, _ = build_model(load_fixture(C5_FIXTURE))
-        model = model.to(gpu)
-        _calibrate(model, _c5_calib_batches(r, 2), gpu)
-        states.append(model)
-    merged = states[0]
-    from qnn.quantize import QuantMeasure, RangeBN
-    with torch.no_grad():
-        for (n, m0), m1 in zip(merged.named_modules(), [m for _, m in states[1].named_modules()]):
-            names = (("running_min", "running_max", "running_mean", "running_var") if isinstance(m0, QuantMeasure)
-                     else ("running_mean", "running_var") if isinstance(m0, RangeBN) else ())
-            for k in names:
-                a, b = getattr(m0, k), getattr(m1, k)
-                a.copy_((a.double() * w[0] + b.double() * w[1]) / (w[0] + w[1]))
-                assert torch.equal(got[0]["state"][n + "." + k if n else k], a.cpu()), f"merged {n}.{k}"
-    del states
+    # every rank holds the same merged calibration after allreduce_calibration (its sample-weighted
+    # merge is checked bitwise against a single-process reconstruction by
+    # test_sharded_engine_world2_device above); the reference engine below is built from it
+    s0, s1 = got[0]["state"], got[1]["state"]
+    assert set(s0) == set(s1)
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), f"ranks disagree on {k} after the merge"
+    merged, _ = build_model(load_fixture(C5_FIXTURE))
+    merged.load_state_dict(s0, strict=True)
+    merged = merged.to(gpu).eval()
     for gb in C5_CASES:
         # rank 1 ran rank 0's tile configuration wherever it is built for its shard
         t0, t1 = got[0][gb]["tiles"], got[1][gb]["tiles"]

@@ -67,7 +67,7 @@ def report(tag, us, nblk, w):
     tot = cyc.sum(-1).mean()
     names = {"rb": ["band", "k-loop", "sums", "staging", "epi", "drain"],
              "rbp": ["chunk0", "k-loop", "sums", "epidata", "epi", "drain"],
-             "rs": ["chunk0", "k-loop", "epiwait", "boxread", "epi", "drain"]}[KERNEL]
+             "rs": ["issue", "wait0", "barrier0", "k-loop", "epi", "drain"]}[KERNEL]
     print(f"== {tag}: {us:.1f} us (stamped build), blocks={nblk}, wave-cycles {tot:.0f}: " +
           "  ".join(f"{a}={m:.0f} ({100 * m / tot:.1f}%)" for a, m in zip(names, mean)))
     if KERNEL == "rs":  # the SIMD pairs: waves 0-3 (priority 1 in the PRIO configurations) vs 4-7
