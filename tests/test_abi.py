@@ -96,7 +96,7 @@ def test_tile_kernel_families(lib):
     fams = [_lib.tile_kernel(k) for k in range(_lib.CONV_TILES)]
     assert set(fams) == {"qconv_kernel", "qconv_pp_kernel", "qconv_band_kernel", "qconv16_kernel",
                          "qconv_rb_kernel", "qconv_direct_kernel", "qconv_rbp_kernel", "qconv_dtab_kernel",
-                         "qconv_pb_kernel"}
+                         "qconv_pb_kernel", "qconv_rs_kernel"}
     # families are contiguous id ranges; round 4 appended the two-team resident band, then the
     # table-epilogue direct configurations (ids of earlier families never move)
     runs = [f for i, f in enumerate(fams) if i == 0 or fams[i - 1] != f]
@@ -110,7 +110,9 @@ def test_tile_kernel_families(lib):
     assert fams[44] == "qconv_direct_kernel"
     # round 5 appended the persistent-band configurations 45-49
     assert _lib.tile_ids("qconv_pb_kernel") == [45, 46, 47, 48, 49]
-    assert [fams[k] for k in range(50, 56)] == ["qconv_kernel"] * 6 and len(fams) == 56
+    assert [fams[k] for k in range(50, 56)] == ["qconv_kernel"] * 6
+    # round 6 appended the streamed resident-band configurations 56-63
+    assert _lib.tile_ids("qconv_rs_kernel") == list(range(56, 64)) and len(fams) == 64
     assert lib.qnn_conv_tile_kernel(-1) is None and lib.qnn_conv_tile_kernel(_lib.CONV_TILES) is None
 
 

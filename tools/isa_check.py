@@ -111,7 +111,7 @@ def smem_lgkm_check(path=LIB):
                     m = LGKM.search(i)
                     if m and int(m.group(1)) == 0:
                         inflight = False
-                    elif m and inflight:
+                    elif m and inflight and int(m.group(1)) < 15:  # lgkmcnt(15): no LGKM wait at all
                         bad.append((name, i))
                 elif op == "s_endpgm":
                     inflight = False
