@@ -94,6 +94,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   // layout): per vector / table array one 4-byte-per-lane DMA per 64 channels, then the EK_LUT
   // code-table rows (1 KiB = 4 rows per 16-byte-per-lane DMA)
   const bool lut_on = EK == EK_LUT && g.lut;
+  const bool lutfast = lut_on && c0 + BM <= d.cout && c0 + BM <= e.code0_cp;  // block-uniform
   int8_t* const epi = smem + p.epi_off;
   const int cw0 = wm * CW;
   const int cmax = d.cout - 1;
@@ -269,7 +270,13 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
           }
           const int m = r0 * d.wo + q, HoWo = d.ho * d.wo;
           const int n = m / HoWo, ho = (m - n * HoWo) / d.wo, wo = m - n * HoWo - ho * d.wo;
-          s_px[q] = make_int4(bx, s_hc[ho] * e.nwc + s_hc[d.ho + wo], m, (n << 16) | (ho << 8) | wo);
+          const int pc = s_hc[ho] * e.nwc + s_hc[d.ho + wo];
+          // the code-table path: the class row's byte offset and the code0 pixel's (32-bit: rs_plan)
+          s_px[q] = lutfast ? make_int4(bx, 4 * (7 + pc) * BM,
+                                        ((n * e.code0_hp + ho + e.code0_pad) * e.code0_wp + wo + e.code0_pad) *
+                                                e.code0_cp + c0,
+                                        bx)
+                            : make_int4(bx, pc, m, (n << 16) | (ho << 8) | wo);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -347,17 +354,96 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
 #if QNN_STAMP
   RB_TS(ts3);
 #endif
-  int sumq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    int q = (wn * TN + j) * 16 + (lane & 15);
-    q = q < npx_blk ? q : npx_blk - 1;
-    sumq[j] = s_px[q].x;
-  }
 #if QNN_STAMP
   RB_TS(ts5);
 #endif
-  {
+  if (lutfast) {
+    // conv -> RangeBN -> ReLU -> next quantizer by the code table, software-pipelined over the
+    // pixel tiles: tile j+1's pixel word and class rows are read while tile j's table bytes are
+    const float* s_f = reinterpret_cast<const float*>(epi);
+    const int8_t* s_lut = epi + 4 * (7 + e.nclass) * BM;
+    const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
+    const int gq = lane >> 4;
+    const int cwl = cw0 + 4 * gq;  // this lane's first local channel of channel tile 0
+    float4 sw[TM], bw[TM], bi[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      sw[i] = *reinterpret_cast<const float4*>(s_f + cwl + 16 * i);
+      bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cwl + 16 * i);
+      bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cwl + 16 * i);
+    }
+    auto pxq = [&](int j) {
+      const int q = (wn * TN + j) * 16 + (lane & 15);
+      return q < npx_blk ? q : npx_blk - 1;  // past the block: the last pixel again (same bytes)
+    };
+    auto rows = [&](int off, float4 (&tb)[TM]) {
+      const float* tp = reinterpret_cast<const float*>(epi + off) + cwl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) tb[i] = *reinterpret_cast<const float4*>(tp + 16 * i);
+    };
+    // LDS returns in order: tile j+1's class rows are requested before tile j's table bytes, and
+    // the pixel word two tiles ahead, so no wait for one tile's rows also waits for its bytes
+    int4 pxc = s_px[pxq(0)];
+    float4 tbc[TM];
+    rows(pxc.y, tbc);
+    int4 pxn = TN > 1 ? s_px[pxq(1)] : pxc;
+    // tile j-1's table bytes are combined and stored after tile j's are requested
+    int bp[TM][4];
+    int8_t* opp = nullptr;
+    auto put = [&](int8_t* op, const int (&b)[TM][4]) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        *reinterpret_cast<int*>(op + 16 * i) = b[i][0] | (b[i][1] << 8) | (b[i][2] << 16) | (b[i][3] << 24);
+    };
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float4 tbn[TM];
+      if (j + 1 < TN) rows(pxn.y, tbn);
+      int4 pxnn = pxn;
+      if (j + 2 < TN) pxnn = s_px[pxq(j + 2)];
+      __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink these reads to their uses)
+      // (.w repeats the sum: a field of the 16-byte read left unused would be reallocated while
+      // the read is in flight, which costs a full lgkmcnt(0) wait)
+      const f2 p2 = {(float)pxc.x, (float)pxc.w};
+      int bq[TM][4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const v4i& a = acc[i][j];
+        const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
+        const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tbc[i].x, tbc[i].y})) +
+                      (f2){bi[i].x, bi[i].y};
+        const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tbc[i].z, tbc[i].w})) +
+                      (f2){bi[i].z, bi[i].w};
+        const f2 q0 = qclamp2(v0, bnp) + MAGIC_U8, q1 = qclamp2(v1, bnp) + MAGIC_U8;
+        const uint8_t* lp = reinterpret_cast<const uint8_t*>(s_lut) + (cwl + 16 * i) * 256;
+        bq[i][0] = lp[__float_as_uint(q0.x) & 255u];
+        bq[i][1] = lp[256 + (__float_as_uint(q0.y) & 255u)];
+        bq[i][2] = lp[512 + (__float_as_uint(q1.x) & 255u)];
+        bq[i][3] = lp[768 + (__float_as_uint(q1.y) & 255u)];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (j > 0) put(opp, bp);
+      opp = e.out_code0 + (uint32_t)pxc.z + cwl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bp[i][k] = bq[i][k];
+      if (j + 1 < TN) {
+        pxc = pxn;
+        pxn = pxnn;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) tbc[i] = tbn[i];
+      }
+    }
+    put(opp, bp);
+  } else {
+    int sumq[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int q = (wn * TN + j) * 16 + (lane & 15);
+      q = q < npx_blk ? q : npx_blk - 1;
+      sumq[j] = s_px[q].x;
+    }
     // this lane's pixel of tile j from the block's pixel table (a slot past the block stands in
     // for the block's last pixel and is never stored)
     auto pixel = [&](int j, q16::Pix& P, int& pc) {
@@ -370,50 +456,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
       P.ho = (px.w >> 8) & 255;
       P.wo = px.w & 255;
     };
-    if (EK == EK_LUT && g.lut && c0 + BM <= d.cout && c0 + BM <= e.code0_cp) {
-      const float* s_f = reinterpret_cast<const float*>(epi);
-      const int8_t* s_lut = epi + 4 * (7 + e.nclass) * BM;
-      const QParams bnp = make_qparams(e.bn_neg_min, e.bn_scale, e.bn_qmax);
-      const int gq = lane >> 4;
-      float4 sw[TM], bw[TM], bi[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int cl_ = cw0 + 16 * i + 4 * gq;
-        sw[i] = *reinterpret_cast<const float4*>(s_f + cl_);
-        bw[i] = *reinterpret_cast<const float4*>(s_f + BM + cl_);
-        bi[i] = *reinterpret_cast<const float4*>(s_f + 2 * BM + cl_);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        q16::Pix P;
-        int pc;
-        pixel(j, P, pc);
-        int8_t* op = e.out_code0 +
-                     (((int64_t)P.n * e.code0_hp + P.ho + e.code0_pad) * e.code0_wp + P.wo + e.code0_pad) * e.code0_cp +
-                     c0 + cw0 + 4 * gq;
-        const float* tp = s_f + (7 + pc) * BM + cw0 + 4 * gq;
-        const f2 p2 = {(float)sumq[j], (float)sumq[j]};
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const float4 tb = *reinterpret_cast<const float4*>(tp + 16 * i);
-          const v4i& a = acc[i][j];
-          const f2 a01 = {(float)a[0], (float)a[1]}, a23 = {(float)a[2], (float)a[3]};
-          const f2 v0 = pfma((f2){sw[i].x, sw[i].y}, a01, pfma((f2){bw[i].x, bw[i].y}, p2, (f2){tb.x, tb.y})) +
-                        (f2){bi[i].x, bi[i].y};
-          const f2 v1 = pfma((f2){sw[i].z, sw[i].w}, a23, pfma((f2){bw[i].z, bw[i].w}, p2, (f2){tb.z, tb.w})) +
-                        (f2){bi[i].z, bi[i].w};
-          const f2 q0 = qclamp2(v0, bnp) + MAGIC_U8, q1 = qclamp2(v1, bnp) + MAGIC_U8;
-          const int8_t* lp = s_lut + (cw0 + 16 * i + 4 * gq) * 256;
-          const int b0_ = (uint8_t)lp[__float_as_uint(q0.x) & 255u];
-          const int b1 = (uint8_t)lp[256 + (__float_as_uint(q0.y) & 255u)];
-          const int b2 = (uint8_t)lp[512 + (__float_as_uint(q1.x) & 255u)];
-          const int b3 = (uint8_t)lp[768 + (__float_as_uint(q1.y) & 255u)];
-          *reinterpret_cast<int*>(op + 16 * i) = b0_ | (b1 << 8) | (b2 << 16) | (b3 << 24);
-        }
-      }
-    } else {
-      q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
-    }
+    q16::epilogue_rb<C, EK>(p, acc, sumq, pixel, smem, c0, wm, lane, g.lut);
   }
 #if QNN_STAMP
   RB_TS(ts6);
@@ -446,7 +489,10 @@ static int rs_plan(const Params& p, Params& q, Geo& g) {
   const int box = 16 * g.npx;  // the pixel table (int4 per output pixel)
   int epi = epi_bytes(p, C::BM);
   g.lut = 0;
-  if (EK == EK_LUT && main + box + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
+  // (the code-table path addresses code0 with 32-bit pixel offsets)
+  const bool off32 = p.e.out_code0 == nullptr ||
+                     (int64_t)p.d.n * p.e.code0_hp * p.e.code0_wp * p.e.code0_cp < ((int64_t)1 << 31);
+  if (EK == EK_LUT && off32 && main + box + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
   if (main + box + epi > LDS_MAX) return -1;
   q.epi_early = 1, q.scr_off = main, q.epi_off = main + box;
   return main + box + epi;
