@@ -30,3 +30,26 @@ def test_no_counted_lgkm_wait_with_scalar_load_in_flight():
     n, bad = isa_check.smem_lgkm_check(LIB)
     assert n >= 100, f"only {n} kernels found: code-object extraction broken?"
     assert not bad, [f"{k[:100]}: {i}" for k, i in bad[:5]]
+
+
+def test_lgkm_hazard_dataflow():
+    """The check follows branches: a counted wait behind a scalar load is flagged on the path that
+    reaches it, a wait only reachable after lgkmcnt(0) or past an unconditional branch is not."""
+    import isa_check
+
+    def prog(lines):
+        return [f"{t}  // {0x1000 + 4 * k:012X}: 00000000" for k, t in enumerate(lines)]
+
+    straight = prog(["s_load_dword s0, s[0:1], 0x0", "ds_read_b32 v0, v1", "s_waitcnt lgkmcnt(1)", "s_endpgm"])
+    assert len(isa_check.lgkm_hazards(straight)) == 1
+    cleared = prog(["s_load_dword s0, s[0:1], 0x0", "s_waitcnt lgkmcnt(0)", "s_waitcnt lgkmcnt(1)", "s_endpgm"])
+    assert isa_check.lgkm_hazards(cleared) == []
+    # k=1 branches over the load to the wait at k=4 (imm 2: next instruction + 2 dwords)
+    skipped = prog(["s_nop 0", "s_branch 2", "s_load_dword s0, s[0:1], 0x0", "s_endpgm",
+                    "s_waitcnt lgkmcnt(1)", "s_endpgm"])
+    assert isa_check.lgkm_hazards(skipped) == []
+    # a backward branch from a load's path into a wait
+    looped = prog(["s_branch 3", "s_waitcnt lgkmcnt(2)", "s_endpgm", "s_nop 0",
+                   "s_load_dword s0, s[0:1], 0x0", "s_branch 65531"])
+    assert len(isa_check.lgkm_hazards(looped)) == 1
+    assert isa_check.lgkm_hazards(prog(["s_load_dword s0, s[0:1], 0x0", "s_waitcnt lgkmcnt(15)", "s_endpgm"])) == []

@@ -91,28 +91,78 @@ if __name__ == "__main__":
     sys.exit(1 if bad else 0)
 
 
+ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+
+
+def _cfg(ins):
+    """Successor lists of one kernel's instructions (branch targets from the objdump addresses;
+    a branch's immediate counts dwords from the next instruction)."""
+    addr = []
+    for i in ins:
+        m = ADDR.search(i)
+        addr.append(int(m.group(1), 16) if m else None)
+    at = {a: k for k, a in enumerate(addr) if a is not None}
+    succ = []
+    for k, i in enumerate(ins):
+        op = i.split()[0]
+        nxt = [k + 1] if k + 1 < len(ins) else []
+        if op == "s_endpgm":
+            succ.append([])
+            continue
+        if op == "s_branch" or op.startswith("s_cbranch"):
+            imm = int(i.split()[1].split("//")[0].strip(","))
+            imm = imm - 65536 if imm >= 32768 else imm
+            base = addr[k + 1] if k + 1 < len(ins) else (addr[k] + 4 if addr[k] is not None else None)
+            t = at.get(base + 4 * imm) if base is not None else None
+            tgt = [t] if t is not None else nxt  # unresolved: fall through (conservative enough)
+            succ.append(tgt if op == "s_branch" else nxt + [t for t in tgt if t not in nxt])
+            continue
+        succ.append(nxt)
+    return succ
+
+
+def lgkm_hazards(ins):
+    """The counted LGKM waits of one kernel's instruction lines reachable with a scalar load in
+    flight (smem_lgkm_check)."""
+    if not ins:
+        return []
+    succ = _cfg(ins)
+    state = [None] * len(ins)  # in-state: a scalar load may be in flight
+    state[0] = False
+    work = [0]
+    while work:
+        k = work.pop()
+        fl = state[k]
+        op = ins[k].split()[0]
+        if op.startswith(SMEM):
+            fl = True
+        elif op == "s_waitcnt":
+            m = LGKM.search(ins[k])
+            if m and int(m.group(1)) == 0:
+                fl = False
+        for t in succ[k]:
+            if state[t] is None or (fl and not state[t]):
+                state[t] = fl or bool(state[t])
+                work.append(t)
+    out = []
+    for k, i in enumerate(ins):
+        if state[k] and i.split()[0] == "s_waitcnt":
+            m = LGKM.search(i)
+            if m and 0 < int(m.group(1)) < 15:  # lgkmcnt(15): no LGKM wait at all
+                out.append(i)
+    return out
+
+
 def smem_lgkm_check(path=LIB):
-    """(kernels scanned, [(kernel, wait)]): every `s_waitcnt lgkmcnt(N > 0)` issued while a
-    scalar-memory load (out-of-order in LGKM_CNT) may still be in flight, in program order (a
-    straight-line scan per kernel; the state clears at lgkmcnt(0)).  The compiler never emits
-    such a wait (with a scalar load pending it waits for 0), so one in the shipped code is a
+    """(kernels scanned, [(kernel, wait)]): every `s_waitcnt lgkmcnt(N)`, 0 < N < 15, that may be
+    reached while a scalar-memory load (out-of-order in LGKM_CNT) is still in flight -- a forward
+    dataflow over the kernel's branches (the state clears at lgkmcnt(0)).  The compiler never
+    emits such a wait (with a scalar load pending it waits for 0), so one in the shipped code is a
     hand-counted inline-asm wait in a window the compiler put a scalar load into (VERDICT r4:
     the resident-band kernels' band reads)."""
     n, bad = 0, []
     for _triple, elf in code_objects(path):
         for name, ins in kernels(elf).items():
             n += 1
-            inflight = False
-            for i in ins:
-                op = i.split()[0]
-                if op.startswith(SMEM):
-                    inflight = True
-                elif op == "s_waitcnt":
-                    m = LGKM.search(i)
-                    if m and int(m.group(1)) == 0:
-                        inflight = False
-                    elif m and inflight and int(m.group(1)) < 15:  # lgkmcnt(15): no LGKM wait at all
-                        bad.append((name, i))
-                elif op == "s_endpgm":
-                    inflight = False
+            bad += [(name, i) for i in lgkm_hazards(ins)]
     return n, bad
