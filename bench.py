@@ -185,7 +185,9 @@ def throughput(global_batch, steps, elapsed):
     return global_batch * steps / elapsed
 
 
-CONV_LAUNCHES = ("qnn_qconv2d_fwd", "qnn_qconv2d_maxpool_fwd")
+# the contractions, and the split residual-chain epilogue of a block's last conv (Engine
+# split_chain): epilogue work moved out of a conv launch is still charged to the contractions
+CONV_LAUNCHES = ("qnn_qconv2d_fwd", "qnn_qconv2d_maxpool_fwd", "qnn_chain_epilogue")
 
 
 def _graph_ms(engine, names, reps):

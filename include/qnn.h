@@ -431,6 +431,17 @@ int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, 
 int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* out_f32,
                       const qnn_code_out* code0, qnn_stream_t stream);
 
+/* The residual-chain tail of a ResNet block's last conv as a launch of its own (the "split"
+ * general epilogue; resnet_quantized.py:60-68 / :105-113 after the conv): bncode holds that
+ * conv's RangeBN input codes [n*ho*wo][c] in the byte C-tile layout (qnn_qconv2d_fwd with
+ * epi->out_bncode, bncode_tiled = 1 and no other output), and this evaluates what the fused
+ * general epilogue computes from them -- RangeBN (epi->bn_*), + the block input (epi->residual
+ * or the chain epi->res[0 .. nres-1], res_relu0), ReLU (epi->relu) -- into epi->out_f32 (C-tile
+ * when f32_tiled, else NHWC) and the codes epi->out_code0 / out_code1 (code*_ fields), bitwise
+ * the fused epilogue's outputs.  The conv-only fields of epi are ignored.  c % 16 == 0. */
+int qnn_chain_epilogue(const uint8_t* bncode, int n, int ho, int wo, int c, const qnn_epilogue* epi,
+                       qnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -537,6 +537,173 @@ static qnn_code_out none_code() {
   return o;
 }
 
+// ------------------------------------------------------------------ split chain epilogue
+// The residual-chain tail of a ResNet block's last conv as its own launch (qnn_chain_epilogue):
+// the conv writes only RangeBN's input codes (EK_BNCODE, byte C-tile), and this kernel -- no
+// MFMA, so four waves per SIMD and packed FP32 -- evaluates everything the fused general
+// epilogue did after the quotient, with the same fp32 ops in the same order (qconv.hip EK_GEN):
+//   v = ((q_bn * s + min - mean) * sq * wq + bq)          RangeBN of the conv's own code
+//   r = residual | chain links (qnn_res_link)             the block input, recomputed
+//   v = relu(v + r); out_f32 = v; codes = quant(v)        (code1 = code0 for equal ranges)
+// One thread per (32x32 tile, lane) = the lane's 16 byte-C-tile values: channels 8g + 4h + u of
+// pixel 32 mt + (lane & 31), h = lane >> 5; a block stays on one channel tile (its RangeBN and
+// link vectors staged once in LDS) and walks pixel tiles.
+__device__ __forceinline__ int4 chain_gather16(int d0, int d1, int d2, int d3) {
+  // lanes 0-31 hold channels 4h.. of groups g; two half-exchange levels leave lanes 0-31 with
+  // channels 0-15 and lanes 32-63 with channels 16-31 of their pixel, in order (qconv.hip gather16)
+  auto r01 = __builtin_amdgcn_permlane32_swap(d0, d1, false, false);
+  auto r23 = __builtin_amdgcn_permlane32_swap(d2, d3, false, false);
+  auto r02 = __builtin_amdgcn_permlane32_swap(r01[0], r23[0], false, false);
+  auto r13 = __builtin_amdgcn_permlane32_swap(r01[1], r23[1], false, false);
+  return make_int4((int)r02[0], (int)r13[0], (int)r02[1], (int)r13[1]);
+}
+
+__global__ __launch_bounds__(256) void chain_epilogue_kernel(const uint8_t* __restrict__ bncode, int n, int ho, int wo,
+                                                             int c, const qnn_epilogue e) {
+  __shared__ float4 s_v[(4 + 4 * QNN_MAX_RES) * 8];  // [vector][32 channels] as float4
+  const int ct = (c + 31) >> 5, ctb = blockIdx.y;
+  const int M = n * ho * wo, mts = (M + 31) >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int nres = e.nres;
+  const int nvec = 4 + 4 * nres;
+  float* sv = reinterpret_cast<float*>(s_v);
+  for (int i = tid; i < nvec * 32; i += 256) {
+    const int v = i >> 5, cc = min(ctb * 32 + (i & 31), c - 1);
+    const float* src;
+    if (v < 4) {
+      src = v == 0 ? e.bn_mean : v == 1 ? e.bn_sq : v == 2 ? e.bn_wq : e.bn_bq;
+    } else {
+      const qnn_res_link& rl = e.res[(v - 4) >> 2];
+      const int k = (v - 4) & 3;
+      src = k == 0 ? rl.mean : k == 1 ? rl.sq : k == 2 ? rl.wq : rl.bq;
+    }
+    sv[i] = src[cc];
+  }
+  __syncthreads();
+  const QParams c0p = make_qparams(e.code0_neg_min, e.code0_scale, e.code0_qmax);
+  const QParams c1p = make_qparams(e.code1_neg_min, e.code1_scale, e.code1_qmax);
+  const bool same01 = e.out_code0 && e.code1_neg_min == e.code0_neg_min && e.code1_scale == e.code0_scale &&
+                      e.code1_qmax == e.code0_qmax;
+  const f2 bn_s2 = {e.bn_scale, e.bn_scale}, bn_m2 = {e.bn_min, e.bn_min};
+  const CodeDst t0 = {e.out_code0, e.code0_cp, e.code0_pad, e.code0_hp, e.code0_wp};
+  const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
+  const int HoWo = ho * wo;
+  for (int mt = blockIdx.x * 4 + (tid >> 6); mt < mts; mt += gridDim.x * 4) {
+    const int64_t off = ((int64_t)mt * ct + ctb) * 1024 + lane * 16;
+    const int m = mt * 32 + (lane & 31);
+    const bool pok = m < M;
+    const int mc = pok ? m : M - 1;
+    const uint4 qb = *reinterpret_cast<const uint4*>(bncode + off);
+    uint4 lq[QNN_MAX_RES];
+#pragma unroll
+    for (int l = 0; l < QNN_MAX_RES; ++l)
+      if (l < nres) lq[l] = *reinterpret_cast<const uint4*>(e.res[l].code + off);
+    int k0[4], k1[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cl = 8 * g + 4 * h;  // local channel of byte 4g (+u)
+      const int cc = ctb * 32 + cl;
+      const bool cok = cc < c;
+      auto vec = [&](int v) { return s_v[v * 8 + (cl >> 2)]; };
+      auto bytes = [](unsigned wd, f2 (&q)[2]) {
+        q[0] = (f2){(float)(wd & 255u), (float)((wd >> 8) & 255u)};
+        q[1] = (f2){(float)((wd >> 16) & 255u), (float)(wd >> 24)};
+      };
+      // RangeBN of the conv's own code (the byte is the rounded quotient: rint2 is the identity)
+      f2 v[2], qq[2];
+      bytes(((const unsigned*)&qb)[g], qq);
+      {
+        const float4 mn4 = vec(0), sq4 = vec(1), wq4 = vec(2), bq4 = vec(3);
+        const f2 mn[2] = {{mn4.x, mn4.y}, {mn4.z, mn4.w}}, sq[2] = {{sq4.x, sq4.y}, {sq4.z, sq4.w}};
+        const f2 wq[2] = {{wq4.x, wq4.y}, {wq4.z, wq4.w}}, bq[2] = {{bq4.x, bq4.y}, {bq4.z, bq4.w}};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          f2 o = qq[hh] * bn_s2;  // dequant: q * s
+          o = o + bn_m2;          // + min
+          o = o - mn[hh];         // x - mean
+          o = o * sq[hh];         // * q(scale)
+          o = o * wq[hh];         // * q(weight)
+          v[hh] = o + bq[hh];     // + q(bias)
+        }
+      }
+      // the block input: fp32, or recomputed from the chain exactly as its producers did
+      auto link = [&](int l, f2 (&o)[2]) {
+        f2 q[2];
+        bytes(((const unsigned*)&lq[l])[g], q);
+        const float4 mn4 = vec(4 + 4 * l), sq4 = vec(5 + 4 * l), wq4 = vec(6 + 4 * l), bq4 = vec(7 + 4 * l);
+        const f2 mn[2] = {{mn4.x, mn4.y}, {mn4.z, mn4.w}}, sq[2] = {{sq4.x, sq4.y}, {sq4.z, sq4.w}};
+        const f2 wq[2] = {{wq4.x, wq4.y}, {wq4.z, wq4.w}}, bq[2] = {{bq4.x, bq4.y}, {bq4.z, bq4.w}};
+        const f2 s2 = {e.res[l].scale, e.res[l].scale}, m2 = {e.res[l].min, e.res[l].min};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          f2 t = q[hh] * s2;
+          t = t + m2;
+          t = t - mn[hh];
+          t = t * sq[hh];
+          t = t * wq[hh];
+          o[hh] = t + bq[hh];
+        }
+      };
+      if (e.residual || nres > 0) {
+        f2 r[2];
+        int l0 = 0;
+        if (e.residual) {
+          const int cr = min(cc, c - 4);
+          const int64_t fi = e.f32_tiled ? ctile_index(mc, cr, ct) : (int64_t)mc * c + cr;
+          const float4 r4 = *reinterpret_cast<const float4*>(e.residual + fi);
+          r[0] = (f2){r4.x, r4.y};
+          r[1] = (f2){r4.z, r4.w};
+        } else {
+          link(0, r);
+          if (e.res_relu0) {
+            r[0].x = fmaxf(r[0].x, 0.f); r[0].y = fmaxf(r[0].y, 0.f);
+            r[1].x = fmaxf(r[1].x, 0.f); r[1].y = fmaxf(r[1].y, 0.f);
+          }
+          l0 = 1;
+        }
+#pragma unroll
+        for (int l = 0; l < QNN_MAX_RES; ++l) {
+          if (l < l0 || l >= nres) continue;
+          f2 o[2];
+          link(l, o);
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const f2 t = o[hh] + r[hh];
+            r[hh].x = fmaxf(t.x, 0.f);
+            r[hh].y = fmaxf(t.y, 0.f);
+          }
+        }
+        v[0] = v[0] + r[0];
+        v[1] = v[1] + r[1];
+      }
+      if (e.relu) {
+        v[0].x = fmaxf(v[0].x, 0.f); v[0].y = fmaxf(v[0].y, 0.f);
+        v[1].x = fmaxf(v[1].x, 0.f); v[1].y = fmaxf(v[1].y, 0.f);
+      }
+      if (e.out_f32 && pok && cok) {
+        const int64_t fi = e.f32_tiled ? ctile_index(m, cc, ct) : (int64_t)m * c + cc;
+        *reinterpret_cast<float4*>(e.out_f32 + fi) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+      }
+      k0[g] = k1[g] = 0;
+      if (e.out_code0 && cok) k0[g] = pack4(qclamp2(v[0], c0p) + MAGIC_S8, qclamp2(v[1], c0p) + MAGIC_S8);
+      if (e.out_code1 && cok)
+        k1[g] = same01 ? k0[g] : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
+    }
+    const int nn = mc / HoWo, hw = mc - nn * HoWo, y = hw / wo, x = hw - y * wo;
+    const int ch = ctb * 32 + 16 * h;
+    if (e.out_code0) {
+      const int4 w4 = chain_gather16(k0[0], k0[1], k0[2], k0[3]);
+      if (pok && ch < t0.cp)
+        *reinterpret_cast<int4*>(t0.ptr + (((int64_t)nn * t0.hp + y + t0.pad) * t0.wp + x + t0.pad) * t0.cp + ch) = w4;
+    }
+    if (e.out_code1) {
+      const int4 w4 = chain_gather16(k1[0], k1[1], k1[2], k1[3]);
+      if (pok && ch < t1.cp)
+        *reinterpret_cast<int4*>(t1.ptr + (((int64_t)nn * t1.hp + y + t1.pad) * t1.wp + x + t1.pad) * t1.cp + ch) = w4;
+    }
+  }
+}
+
 static int check_code(const qnn_code_out* o, int c, const char* what) {
   if (!o || !o->ptr) return QNN_OK;
   if (o->cp < c || o->cp % 4 || o->scale <= 0.f || o->pad < 0 || (((uintptr_t)o->ptr) & 3))
@@ -687,6 +854,40 @@ int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, 
   QNN_REQUIRE(bn && lut && code0 && code0->ptr, "qnn_dwconv_fused_lut: RangeBN, its code table and a code output");
   return dwconv_fused(x, n, h, w, pad, hp, wp, cp, c, w_hat_t, kh, kw, sh, sw, ho, wo, x_min, x_scale, bias, bn, 1,
                       nullptr, code0, stream, false, lut);
+}
+
+int qnn_chain_epilogue(const uint8_t* bncode, int n, int ho, int wo, int c, const qnn_epilogue* epi,
+                       qnn_stream_t stream) {
+  QNN_REQUIRE(epi, "null epilogue");
+  const qnn_epilogue& e = *epi;
+  QNN_REQUIRE(n >= 0 && ho > 0 && wo > 0 && c > 0 && c % 16 == 0, "bad shape (c % 16 == 0)");
+  QNN_REQUIRE(e.bn_mean && e.bn_sq && e.bn_wq && e.bn_bq && e.bn_scale > 0.f, "bad RangeBN params");
+  QNN_REQUIRE(e.nres >= 0 && e.nres <= QNN_MAX_RES, "nres out of range");
+  for (int l = 0; l < e.nres; ++l)
+    QNN_REQUIRE(e.res[l].code && (((uintptr_t)e.res[l].code) & 15) == 0 && e.res[l].mean && e.res[l].sq &&
+                    e.res[l].wq && e.res[l].bq,
+                "bad residual link (16-byte aligned codes, all vectors)");
+  QNN_REQUIRE(e.out_f32 || e.out_code0 || e.out_code1, "no output");
+  QNN_REQUIRE(!e.out_f32 || (((uintptr_t)e.out_f32) & 15) == 0, "out_f32 must be 16-byte aligned");
+  QNN_REQUIRE(!e.residual || (((uintptr_t)e.residual) & 15) == 0, "residual must be 16-byte aligned");
+  auto code16 = [&](const int8_t* p, int cp, int pad, float scale) {
+    return !p || (cp >= c && cp % 16 == 0 && pad >= 0 && scale > 0.f && (((uintptr_t)p) & 15) == 0);
+  };
+  QNN_REQUIRE(code16(e.out_code0, e.code0_cp, e.code0_pad, e.code0_scale) &&
+                  code16(e.out_code1, e.code1_cp, e.code1_pad, e.code1_scale),
+              "bad code output (cp % 16, 16-B aligned)");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(bncode && (((uintptr_t)bncode) & 15) == 0, "bncode must be non-null and 16-byte aligned");
+  const int64_t M = (int64_t)n * ho * wo;
+  QNN_REQUIRE(M < ((int64_t)1 << 31), "n * ho * wo >= 2^31");
+  const int64_t mts = (M + 31) / 32;
+  const int ct = (c + 31) / 32;
+  // about 8 blocks per CU over the channel tiles, each walking pixel tiles four at a time
+  const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(cdiv(mts, 4), cdiv(256 * 8, ct)));
+  hipLaunchKernelGGL(chain_epilogue_kernel, dim3((unsigned)gx, (unsigned)ct), dim3(256), 0, (hipStream_t)stream,
+                     bncode, n, ho, wo, c, e);
+  QNN_LAUNCH_CHECK("qnn_chain_epilogue");
+  return QNN_OK;
 }
 
 int qnn_bn_code_lut(const qnn_bn_params* bn, int c, int relu, const qnn_code_out* next, int8_t* lut,

@@ -249,6 +249,69 @@ __global__ __launch_bounds__(256) void quantize_s2d_x2_kernel(const float* __res
     *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
+// quantize_s2d_x2_kernel's codes with one wave per s2d row (lane k = pair k of the row, wz2 <= 64):
+// the row's image and height come from the wave-uniform row index on the scalar unit, so no lane
+// divides (the grid-stride form spent ~3 64-bit divisions per pair), and the tail zero page is
+// written by the first block.  Bitwise quantize_s2d_x2_kernel's (same loads, same quotients).
+template <int OFF, int CH>
+__global__ __launch_bounds__(256) void quantize_s2d_rows_kernel(const float* __restrict__ x, int8_t* __restrict__ z,
+                                                                int n, int h, int w, int pad, int hz, int wz,
+                                                                float neg_min, float scale, float qmax) {
+  constexpr int c = CH;
+  constexpr int off = OFF;
+  const float inv = 1.0f / scale;
+  const int wz2 = (wz + 1) >> 1;
+  const int r = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // s2d row (img, h2)
+  const int k = threadIdx.x & 63;
+  if (r < n * hz && k < wz2) {
+    const int img = r / hz, h2 = r - img * hz;
+    const int64_t hw = (int64_t)h * w;
+    const int w4 = w >> 2;
+    const int a = (4 * k - pad - off) >> 2;
+    float v[2][4][4];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int iy = 2 * h2 + rr - pad;
+      const bool rok = iy >= 0 && iy < h;
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) {
+        float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+        if (ci < c && rok) {
+          const float4* row = reinterpret_cast<const float4*>(x + ((int64_t)img * c + ci) * hw + (int64_t)iy * w);
+          if (a >= 0 && a < w4) A = row[a];
+          if (a + 1 >= 0 && a + 1 < w4) B = row[a + 1];
+        }
+        const float e[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[rr][ci][j] = e[off + j];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int w2 = 2 * k + p;
+      if (w2 >= wz) break;
+      union {
+        int8_t b[16];
+        int4 q;
+      } out;
+      out.q = make_int4(0, 0, 0, 0);
+#pragma unroll
+      for (int uv = 0; uv < 4; ++uv) {
+        const int rr = uv >> 1, u = uv & 1;
+        const int iy = 2 * h2 + rr - pad, ix = 2 * w2 + u - pad;
+        const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci)
+          if (ci < c && ok)
+            out.b[uv * c + ci] = (int8_t)((int)quant_code_fast(v[rr][ci][2 * p + u], neg_min, scale, inv, qmax) - 128);
+      }
+      *reinterpret_cast<int4*>(z + ((int64_t)r * wz + w2) * 16) = out.q;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 8)
+    *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
+}
+
 // ------------------------------------------------------------------ gradient quantizer
 // quantize.py:76-97 with enforce_true_zero (the binding of UniformQuantizeGrad.backward):
 // the reference's in-place op order, one element per lane, four per thread
@@ -605,8 +668,20 @@ int qnn_quantize_nchw_to_s2d8(const float* x, int8_t* z, int n, int c, int h, in
   if (w % 4 == 0 && (((uintptr_t)x) & 15) == 0) {
     const int64_t pairs = (int64_t)n * hz * ((wz + 1) / 2);
     const dim3 grid(grid_for(pairs > 0 ? pairs : 1, 256));
+    const int64_t rows = (int64_t)n * hz;
+    const bool by_rows = (wz + 1) / 2 <= 64 && rows < ((int64_t)1 << 30);
+    const dim3 grid_rows((unsigned)(rows > 0 ? (rows + 3) / 4 : 1));
     auto go = [&](auto offc) {
       constexpr int O = decltype(offc)::value;
+      if (by_rows) {
+        switch (c) {
+          case 1: hipLaunchKernelGGL((quantize_s2d_rows_kernel<O, 1>), grid_rows, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+          case 2: hipLaunchKernelGGL((quantize_s2d_rows_kernel<O, 2>), grid_rows, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+          case 3: hipLaunchKernelGGL((quantize_s2d_rows_kernel<O, 3>), grid_rows, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+          default: hipLaunchKernelGGL((quantize_s2d_rows_kernel<O, 4>), grid_rows, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
+        }
+        return;
+      }
       switch (c) {
         case 1: hipLaunchKernelGGL((quantize_s2d_x2_kernel<O, 1>), grid, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;
         case 2: hipLaunchKernelGGL((quantize_s2d_x2_kernel<O, 2>), grid, dim3(256), 0, (hipStream_t)stream, x, z, n, h, w, pad, hz, wz, neg_min, scale, qmax); break;

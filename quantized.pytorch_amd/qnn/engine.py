@@ -78,7 +78,7 @@ class Engine:
     TIE = 0.02  # autotune: timings within 2 % of the fastest count as a tie (lowest configuration id wins)
 
     def __init__(self, model, batch, input_hw=None, graph=True, autotune=True, tile=None, fuse_stem_pool=True,
-                 max_links=None, tiles=None, branches=None):
+                 max_links=None, tiles=None, branches=None, split_chain=None):
         """tile=k forces tile configuration k on every contraction it is built for (the
         others keep the cost model's choice); tile=None autotunes (or the cost model
         when autotune=False).  QNN_ENGINE_TILES="k,k,..." fixes every conv's tile.
@@ -96,8 +96,15 @@ class Engine:
         buffer or read one the other writes).  Measured slower (ResNet-18 b128 160.1 K vs 164.2 K
         img/s serial, ResNet-50 b256 56.8 K vs 57.2 K): the graph's fork/join edges widen the
         gaps between launches (trace busy time 0.760 of 0.830 ms per forward, against 0.794 of
-        0.815 serial) by more than the overlap saves, so the serial order is the default."""
+        0.815 serial) by more than the overlap saves, so the serial order is the default.
+        split_chain: each ResNet block's last conv writes only its RangeBN input codes and the
+        residual-chain tail (RangeBN, + the block input, ReLU, the consumers' codes) runs as a
+        launch of its own (qnn_chain_epilogue: no MFMA, full occupancy, packed FP32) instead of
+        in the conv's epilogue; bitwise the same outputs.  None = QNN_ENGINE_SPLIT_CHAIN."""
         self.fuse_stem_pool = fuse_stem_pool
+        if split_chain is None:
+            split_chain = os.environ.get("QNN_ENGINE_SPLIT_CHAIN", "0") == "1"
+        self.split_chain = bool(split_chain)
         if branches is None:
             branches = os.environ.get("QNN_ENGINE_BRANCHES", "0") == "1"
         self.branches = bool(branches)
@@ -280,23 +287,9 @@ class Engine:
                 b = self._bn(bn)
                 e.bn_mean, e.bn_sq, e.bn_wq, e.bn_bq = b.mean, b.sq, b.wq, b.bq
                 e.bn_neg_min, e.bn_min, e.bn_scale, e.bn_qmax = b.neg_min, b.min, b.scale, b.qmax
-            if chain is not None:
-                f32, links, relu0 = chain
-                e.residual = None if f32 is None else f32.data_ptr()
-                e.nres, e.res_relu0 = len(links), (1 if relu0 and f32 is None else 0)
-                for l, (code, lbn) in enumerate(links):
-                    lb = self._bn(lbn)
-                    e.res[l] = _lib.ResLink(code=code.data_ptr(), mean=lb.mean, sq=lb.sq, wq=lb.wq, bq=lb.bq,
-                                            min=lb.min, scale=lb.scale)
+            self._chain_fields(e, chain, relu, outs, out_f32)
             e.bncode_tiled = 1 if bncode_tiled else 0
-            e.relu = 1 if relu else 0
-            e.out_f32 = None if out_f32 is None else out_f32.data_ptr()
             e.out_bncode = None if out_bncode is None else out_bncode.data_ptr()
-            for k, co in enumerate(outs[:2]):
-                for f in ("cp", "pad", "hp", "wp", "neg_min", "scale", "qmax"):
-                    setattr(e, f"code{k}_{f}", getattr(co, f))
-                setattr(e, f"out_code{k}", co.ptr)
-            assert len(outs) <= 2
             if bn is not None and chain is None and out_f32 is None and out_bncode is None and len(outs) == 1:
                 # conv -> RangeBN -> ReLU -> consumer quantizer: one exact per-channel code table
                 lut = torch.empty((cout, 256), dtype=torch.int8, device=self.dev)
@@ -331,6 +324,50 @@ class Engine:
         self._add("qnn_qconv2d_fwd", lambda st: _lib.call("qnn_qconv2d_fwd", xp, wp_, dp, ep, st), ops, nbytes,
                   [M, cout, kh * kw * cin])
         return Ho, Wo
+
+    def _chain_fields(self, e, chain, relu, outs, out_f32):
+        """The residual, ReLU and output fields of a mode-1 epilogue (fused or split)."""
+        if chain is not None:
+            f32, links, relu0 = chain
+            e.residual = None if f32 is None else f32.data_ptr()
+            e.nres, e.res_relu0 = len(links), (1 if relu0 and f32 is None else 0)
+            for l, (code, lbn) in enumerate(links):
+                lb = self._bn(lbn)
+                e.res[l] = _lib.ResLink(code=code.data_ptr(), mean=lb.mean, sq=lb.sq, wq=lb.wq, bq=lb.bq,
+                                        min=lb.min, scale=lb.scale)
+        e.relu = 1 if relu else 0
+        e.out_f32 = None if out_f32 is None else out_f32.data_ptr()
+        assert len(outs) <= 2
+        for k, co in enumerate(outs[:2]):
+            for f in ("cp", "pad", "hp", "wp", "neg_min", "scale", "qmax"):
+                setattr(e, f"code{k}_{f}", getattr(co, f))
+            setattr(e, f"out_code{k}", co.ptr)
+
+    def _conv_chain(self, conv, src, H, W, Ho, Wo, bn, chain, outs, out_f32, out_bncode):
+        """A block's last conv: RangeBN, + the block input (chain), ReLU, the consumers' codes, the
+        fp32 map (out_f32) and its own RangeBN codes as the next chain link (out_bncode) -- fused in
+        the conv's general epilogue, or (split_chain) as the conv's RangeBN codes and one
+        qnn_chain_epilogue launch over them (resnet_quantized.py:60-68 / :105-113)."""
+        if not self.split_chain:
+            self._conv(conv, src, H, W, bn=bn, chain=chain, relu=True, outs=outs, out_f32=out_f32,
+                       out_bncode=out_bncode, bncode_tiled=True)
+            return
+        cout = conv.out_channels
+        code = out_bncode if out_bncode is not None else self._btiled(Ho, Wo, cout)
+        self._conv(conv, src, H, W, bn=bn, relu=False, out_bncode=code, bncode_tiled=True)
+        e = _lib.Epilogue()
+        e.mode, e.f32_tiled = 1, 1
+        b = self._bn(bn)
+        e.bn_mean, e.bn_sq, e.bn_wq, e.bn_bq = b.mean, b.sq, b.wq, b.bq
+        e.bn_neg_min, e.bn_min, e.bn_scale, e.bn_qmax = b.neg_min, b.min, b.scale, b.qmax
+        self._chain_fields(e, chain, True, outs, out_f32)
+        self.keep += [e, code]
+        N, cp_, ep = self.N, _lib.ptr(code), ctypes.byref(e)
+        M = N * Ho * Wo
+        nbytes = M * cout * (1 + len(outs) + (4 if out_f32 is not None else 0) +
+                             (4 if chain[0] is not None else 0) + len(chain[1]))
+        self._add("qnn_chain_epilogue", lambda st: _lib.call("qnn_chain_epilogue", cp_, N, Ho, Wo, cout, ep, st),
+                  0, nbytes, [M, cout])
 
     # ------------------------------------------------------------------ ResNet
     @staticmethod
@@ -493,14 +530,12 @@ class Engine:
             a2 = _Act(Ho, Wo, blk.conv2.out_channels)
             self._conv(blk.conv2, self._codes_for(a1, blk.conv2), x.H, x.W, bn=blk.bn2, relu=True,
                        outs=[self._codes_for(a2, blk.conv3)[1]])
-            self._conv(blk.conv3, self._codes_for(a2, blk.conv3), Ho, Wo, bn=blk.bn3, chain=chain, relu=True,
-                       outs=outs, out_f32=f32, out_bncode=bnc, bncode_tiled=True)
+            self._conv_chain(blk.conv3, self._codes_for(a2, blk.conv3), Ho, Wo, Ho, Wo, blk.bn3, chain, outs, f32, bnc)
         else:
             a1 = _Act(Ho, Wo, blk.conv1.out_channels)
             self._conv(blk.conv1, self._codes_for(x, blk.conv1), x.H, x.W, bn=blk.bn1, relu=True,
                        outs=[self._codes_for(a1, blk.conv2)[1]])
-            self._conv(blk.conv2, self._codes_for(a1, blk.conv2), Ho, Wo, bn=blk.bn2, chain=chain, relu=True,
-                       outs=outs, out_f32=f32, out_bncode=bnc, bncode_tiled=True)
+            self._conv_chain(blk.conv2, self._codes_for(a1, blk.conv2), Ho, Wo, Ho, Wo, blk.bn2, chain, outs, f32, bnc)
         if ds_op is not None:  # the downsample's codes are read first by the block's last conv
             self.forks[ds_op] = len(self.ops) - 1
         return out

@@ -237,3 +237,21 @@ def test_engine_bench_batch_bitwise_c3_c4(gpu, fixture, batch):
         assert multi and max(multi) >= 2, f"no direct-fragment launch loops over >= 2 tiles per block: {multi}"
     # the logits too: the engine's avg-pool sums in torch's AvgPool2d order
     assert torch.equal(out, logits), (out - logits).abs().max().item()
+
+
+@pytest.mark.parametrize("fixture,batch", [("model_resnet50_imagenet", 256), ("model_resnet18_imagenet", 128)])
+def test_engine_split_chain_bench_batch_bitwise(gpu, fixture, batch):
+    """The split residual-chain epilogue (qnn_chain_epilogue) at the bench batches (C2, C3):
+    the launch walks many pixel tiles per block; head input and logits bitwise the module path."""
+    from qnn.engine import Engine
+    d = load_fixture(fixture)
+    model, _ = build_model(d)
+    x = synthetic.input_batch((batch,) + tuple(d["config"]["shape"][1:]), 94)
+    model = model.to(gpu)
+    xg = x.to(gpu)
+    logits, feat = _module_feat(model, xg)
+    eng = Engine(model, batch=batch, split_chain=True)
+    out = eng(xg)
+    assert "qnn_chain_epilogue" in eng.launch_names
+    assert torch.equal(eng.head_input, feat.permute(0, 2, 3, 1)), "split-chain engine != module path"
+    assert torch.equal(out, logits)

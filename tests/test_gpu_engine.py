@@ -112,3 +112,23 @@ def test_engine_chain_length_bitwise(gpu, name, max_links):
     eng = Engine(model, batch=x.shape[0], max_links=max_links)
     eng(xg)
     assert torch.equal(eng.head_input, mod_feat.permute(0, 2, 3, 1)), f"max_links={max_links}: != module path"
+
+
+@pytest.mark.parametrize("max_links", [0, 2, 4])
+@pytest.mark.parametrize("name", ["resnet18_imagenet", "resnet50_imagenet", "resnet18_cifar"])
+def test_engine_split_chain_bitwise(gpu, name, max_links):
+    """The residual-chain tail of every block's last conv as its own launch
+    (qnn_chain_epilogue, Engine(split_chain=True)) gives the same head input and logits as
+    the fused general epilogue, bitwise, at every chain length (fp32 checkpoints, links)."""
+    d = load_fixture("model_" + name)
+    model, x = build_model(d)
+    model = model.to(gpu)
+    xg = x.to(gpu)
+    fused = Engine(model, batch=x.shape[0], max_links=max_links, split_chain=False, autotune=False)
+    yf = fused(xg).clone()
+    hf = fused.head_input.clone()
+    split = Engine(model, batch=x.shape[0], max_links=max_links, split_chain=True, autotune=False)
+    assert split.launch_names.count("qnn_chain_epilogue") == len(Engine._blocks(model))
+    ys = split(xg)
+    assert torch.equal(split.head_input, hf)
+    assert torch.equal(ys, yf)

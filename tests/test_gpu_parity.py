@@ -99,6 +99,9 @@ def test_activation_codes_padded_nhwc8(gpu, shape, c_pad, pad):
     (36, 32, 3, 20, 19),     # w % 4 == 0: two per thread (aligned float4 pairs), 7x7/2 stem padding, odd wz
     (36, 32, 1, 18, 17),     # MobileNet's 3x3/2 stem padding
     (40, 40, 2, 22, 22),     # even padding
+    (224, 224, 3, 115, 115),  # the ResNet stem at 224 (one wave per s2d row)
+    (224, 224, 1, 113, 113),  # the MobileNet stem at 224 (odd hz, wz)
+    (12, 264, 3, 9, 135),    # more than 64 pairs per row: the grid-stride form
 ])
 def test_activation_codes_space_to_depth(gpu, H, W, pad, hz, wz):
     N, C = 2, 3

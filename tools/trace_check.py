@@ -15,14 +15,14 @@ concurrently with the main path, so launches may overlap), the contraction kerne
 the roofline fraction Σ contraction ops / their busy time / peak.  It FAILS (exit 1) when the
 trace's per-forward busy time exceeds the bench's own ms_per_step (the trace would then not
 describe the benched build), or when the bench's roofline.frac differs from the trace's by more
-than 5 % (relative).  Contraction kernels: qconv*/stem_pool*.
+than 5 % (relative).  Contraction kernels: qconv*/stem_pool*/chain_epilogue*.
 """
 import csv
 import json
 import sys
 
 PEAK_TOPS = 5000.0
-CONV_KERNELS = ("qconv", "stem_pool")
+CONV_KERNELS = ("qconv", "stem_pool", "chain_epilogue")  # (the split chain epilogue: charged to the contractions)
 
 
 def forward_blocks(rows, period):
