@@ -558,13 +558,16 @@ __device__ __forceinline__ int4 chain_gather16(int d0, int d1, int d2, int d3) {
   return make_int4((int)r02[0], (int)r13[0], (int)r02[1], (int)r13[1]);
 }
 
-__global__ __launch_bounds__(256) void chain_epilogue_kernel(const uint8_t* __restrict__ bncode, int n, int ho, int wo,
-                                                             int c, const qnn_epilogue e) {
+// NRES links and RES (an fp32 checkpoint as the block input) are compile-time, so a launch
+// carries only its chain (no runtime-branched link loop, no scalar spills); four waves per SIMD.
+template <int NRES, bool RES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void chain_epilogue_kernel(
+    const uint8_t* __restrict__ bncode, int n, int ho, int wo, int c, const qnn_epilogue e) {
   __shared__ float4 s_v[(4 + 4 * QNN_MAX_RES) * 8];  // [vector][32 channels] as float4
   const int ct = (c + 31) >> 5, ctb = blockIdx.y;
   const int M = n * ho * wo, mts = (M + 31) >> 5;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
-  const int nres = e.nres;
+  constexpr int nres = NRES;
   const int nvec = 4 + 4 * nres;
   float* sv = reinterpret_cast<float*>(s_v);
   for (int i = tid; i < nvec * 32; i += 256) {
@@ -590,6 +593,10 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(const uint8_t* __re
   const int HoWo = ho * wo;
   for (int mt = blockIdx.x * 4 + (tid >> 6); mt < mts; mt += gridDim.x * 4) {
     const int64_t off = ((int64_t)mt * ct + ctb) * 1024 + lane * 16;
+    // the staged vectors are re-read per pixel tile: an opaque base keeps the compiler from
+    // hoisting all (4 + 4 nres) x 16 of them into registers for the whole loop
+    int vb = 0;
+    asm volatile("" : "+v"(vb));
     const int m = mt * 32 + (lane & 31);
     const bool pok = m < M;
     const int mc = pok ? m : M - 1;
@@ -604,7 +611,7 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(const uint8_t* __re
       const int cl = 8 * g + 4 * h;  // local channel of byte 4g (+u)
       const int cc = ctb * 32 + cl;
       const bool cok = cc < c;
-      auto vec = [&](int v) { return s_v[v * 8 + (cl >> 2)]; };
+      auto vec = [&](int v) { return s_v[vb + v * 8 + (cl >> 2)]; };
       auto bytes = [](unsigned wd, f2 (&q)[2]) {
         q[0] = (f2){(float)(wd & 255u), (float)((wd >> 8) & 255u)};
         q[1] = (f2){(float)((wd >> 16) & 255u), (float)(wd >> 24)};
@@ -644,10 +651,10 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(const uint8_t* __re
           o[hh] = t + bq[hh];
         }
       };
-      if (e.residual || nres > 0) {
+      if (RES || nres > 0) {
         f2 r[2];
         int l0 = 0;
-        if (e.residual) {
+        if (RES) {
           const int cr = min(cc, c - 4);
           const int64_t fi = e.f32_tiled ? ctile_index(mc, cr, ct) : (int64_t)mc * c + cr;
           const float4 r4 = *reinterpret_cast<const float4*>(e.residual + fi);
@@ -884,8 +891,21 @@ int qnn_chain_epilogue(const uint8_t* bncode, int n, int ho, int wo, int c, cons
   const int ct = (c + 31) / 32;
   // about 8 blocks per CU over the channel tiles, each walking pixel tiles four at a time
   const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(cdiv(mts, 4), cdiv(256 * 8, ct)));
-  hipLaunchKernelGGL(chain_epilogue_kernel, dim3((unsigned)gx, (unsigned)ct), dim3(256), 0, (hipStream_t)stream,
-                     bncode, n, ho, wo, c, e);
+  const dim3 grid((unsigned)gx, (unsigned)ct);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, bncode, n, ho, wo, c, e); };
+  const bool res = e.residual != nullptr;
+  switch (e.nres * 2 + (res ? 1 : 0)) {
+    case 0: go(chain_epilogue_kernel<0, false>); break;
+    case 1: go(chain_epilogue_kernel<0, true>); break;
+    case 2: go(chain_epilogue_kernel<1, false>); break;
+    case 3: go(chain_epilogue_kernel<1, true>); break;
+    case 4: go(chain_epilogue_kernel<2, false>); break;
+    case 5: go(chain_epilogue_kernel<2, true>); break;
+    case 6: go(chain_epilogue_kernel<3, false>); break;
+    case 7: go(chain_epilogue_kernel<3, true>); break;
+    case 8: go(chain_epilogue_kernel<4, false>); break;
+    default: go(chain_epilogue_kernel<4, true>); break;
+  }
   QNN_LAUNCH_CHECK("qnn_chain_epilogue");
   return QNN_OK;
 }
