@@ -560,9 +560,12 @@ __device__ __forceinline__ int4 chain_gather16(int d0, int d1, int d2, int d3) {
 
 // NRES links and RES (an fp32 checkpoint as the block input) are compile-time, so a launch
 // carries only its chain (no runtime-branched link loop, no scalar spills); four waves per SIMD.
-template <int NRES, bool RES>
+// FULL: c % 32 == 0, every channel of a tile exists (no per-group channel tests).
+// (dx, dy, dn): a wave's pixel step between its tiles (32 * 4 * gridDim.x pixels) as columns,
+// rows and images, so each lane's output coordinates advance by adds, not divisions.
+template <int NRES, bool RES, bool FULL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void chain_epilogue_kernel(
-    const uint8_t* __restrict__ bncode, int n, int ho, int wo, int c, const qnn_epilogue e) {
+    const uint8_t* __restrict__ bncode, int n, int ho, int wo, int c, int dx, int dy, int dn, const qnn_epilogue e) {
   __shared__ float4 s_v[(4 + 4 * QNN_MAX_RES) * 8];  // [vector][32 channels] as float4
   const int ct = (c + 31) >> 5, ctb = blockIdx.y;
   const int M = n * ho * wo, mts = (M + 31) >> 5;
@@ -591,6 +594,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   const CodeDst t0 = {e.out_code0, e.code0_cp, e.code0_pad, e.code0_hp, e.code0_wp};
   const CodeDst t1 = {e.out_code1, e.code1_cp, e.code1_pad, e.code1_hp, e.code1_wp};
   const int HoWo = ho * wo;
+  int nn, y, x;  // this lane's output pixel (image, row, column), advanced per tile
+  {
+    const int m0 = (blockIdx.x * 4 + (tid >> 6)) * 32 + (lane & 31);
+    nn = m0 / HoWo;
+    y = (m0 - nn * HoWo) / wo;
+    x = m0 - nn * HoWo - y * wo;
+  }
   for (int mt = blockIdx.x * 4 + (tid >> 6); mt < mts; mt += gridDim.x * 4) {
     const int64_t off = ((int64_t)mt * ct + ctb) * 1024 + lane * 16;
     // the staged vectors are re-read per pixel tile: an opaque base keeps the compiler from
@@ -610,7 +620,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     for (int g = 0; g < 4; ++g) {
       const int cl = 8 * g + 4 * h;  // local channel of byte 4g (+u)
       const int cc = ctb * 32 + cl;
-      const bool cok = cc < c;
+      const bool cok = FULL || cc < c;
       auto vec = [&](int v) { return s_v[vb + v * 8 + (cl >> 2)]; };
       auto bytes = [](unsigned wd, f2 (&q)[2]) {
         q[0] = (f2){(float)(wd & 255u), (float)((wd >> 8) & 255u)};
@@ -696,7 +706,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       if (e.out_code1 && cok)
         k1[g] = same01 ? k0[g] : pack4(qclamp2(v[0], c1p) + MAGIC_S8, qclamp2(v[1], c1p) + MAGIC_S8);
     }
-    const int nn = mc / HoWo, hw = mc - nn * HoWo, y = hw / wo, x = hw - y * wo;
     const int ch = ctb * 32 + 16 * h;
     if (e.out_code0) {
       const int4 w4 = chain_gather16(k0[0], k0[1], k0[2], k0[3]);
@@ -708,6 +717,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       if (pok && ch < t1.cp)
         *reinterpret_cast<int4*>(t1.ptr + (((int64_t)nn * t1.hp + y + t1.pad) * t1.wp + x + t1.pad) * t1.cp + ch) = w4;
     }
+    x += dx;
+    y += dy;
+    nn += dn;
+    if (x >= wo) x -= wo, ++y;
+    if (y >= ho) y -= ho, ++nn;
   }
 }
 
@@ -892,20 +906,30 @@ int qnn_chain_epilogue(const uint8_t* bncode, int n, int ho, int wo, int c, cons
   // about 8 blocks per CU over the channel tiles, each walking pixel tiles four at a time
   const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(cdiv(mts, 4), cdiv(256 * 8, ct)));
   const dim3 grid((unsigned)gx, (unsigned)ct);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, bncode, n, ho, wo, c, e); };
+  const int64_t step = 32 * 4 * gx;  // pixels between a wave's tiles
+  const int dx = (int)(step % wo), rows = (int)(step / wo), dy = rows % ho, dn = rows / ho;
+  const bool full = c % 32 == 0;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, bncode, n, ho, wo, c, dx, dy, dn, e);
+  };
   const bool res = e.residual != nullptr;
-  switch (e.nres * 2 + (res ? 1 : 0)) {
-    case 0: go(chain_epilogue_kernel<0, false>); break;
-    case 1: go(chain_epilogue_kernel<0, true>); break;
-    case 2: go(chain_epilogue_kernel<1, false>); break;
-    case 3: go(chain_epilogue_kernel<1, true>); break;
-    case 4: go(chain_epilogue_kernel<2, false>); break;
-    case 5: go(chain_epilogue_kernel<2, true>); break;
-    case 6: go(chain_epilogue_kernel<3, false>); break;
-    case 7: go(chain_epilogue_kernel<3, true>); break;
-    case 8: go(chain_epilogue_kernel<4, false>); break;
-    default: go(chain_epilogue_kernel<4, true>); break;
-  }
+  auto pick = [&](auto fullc) {
+    constexpr bool F = decltype(fullc)::value;
+    switch (e.nres * 2 + (res ? 1 : 0)) {
+      case 0: go(chain_epilogue_kernel<0, false, F>); break;
+      case 1: go(chain_epilogue_kernel<0, true, F>); break;
+      case 2: go(chain_epilogue_kernel<1, false, F>); break;
+      case 3: go(chain_epilogue_kernel<1, true, F>); break;
+      case 4: go(chain_epilogue_kernel<2, false, F>); break;
+      case 5: go(chain_epilogue_kernel<2, true, F>); break;
+      case 6: go(chain_epilogue_kernel<3, false, F>); break;
+      case 7: go(chain_epilogue_kernel<3, true, F>); break;
+      case 8: go(chain_epilogue_kernel<4, false, F>); break;
+      default: go(chain_epilogue_kernel<4, true, F>); break;
+    }
+  };
+  if (full) pick(std::true_type{});
+  else pick(std::false_type{});
   QNN_LAUNCH_CHECK("qnn_chain_epilogue");
   return QNN_OK;
 }
