@@ -601,8 +601,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     y = (m0 - nn * HoWo) / wo;
     x = m0 - nn * HoWo - y * wo;
   }
-  for (int mt = blockIdx.x * 4 + (tid >> 6); mt < mts; mt += gridDim.x * 4) {
-    const int64_t off = ((int64_t)mt * ct + ctb) * 1024 + lane * 16;
+  // the next tile's code bytes are requested before this tile's arithmetic (one tile ahead)
+  const int stride = gridDim.x * 4;
+  int mt = blockIdx.x * 4 + (tid >> 6);
+  uint4 qbn = make_uint4(0, 0, 0, 0), lqn[QNN_MAX_RES];
+  auto fetch = [&](int t) {
+    const int64_t o = ((int64_t)t * ct + ctb) * 1024 + lane * 16;
+    qbn = *reinterpret_cast<const uint4*>(bncode + o);
+#pragma unroll
+    for (int l = 0; l < QNN_MAX_RES; ++l)
+      if (l < nres) lqn[l] = *reinterpret_cast<const uint4*>(e.res[l].code + o);
+  };
+  if (mt < mts) fetch(mt);
+  for (; mt < mts; mt += stride) {
     // the staged vectors are re-read per pixel tile: an opaque base keeps the compiler from
     // hoisting all (4 + 4 nres) x 16 of them into registers for the whole loop
     int vb = 0;
@@ -610,11 +621,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     const int m = mt * 32 + (lane & 31);
     const bool pok = m < M;
     const int mc = pok ? m : M - 1;
-    const uint4 qb = *reinterpret_cast<const uint4*>(bncode + off);
+    const uint4 qb = qbn;
     uint4 lq[QNN_MAX_RES];
 #pragma unroll
     for (int l = 0; l < QNN_MAX_RES; ++l)
-      if (l < nres) lq[l] = *reinterpret_cast<const uint4*>(e.res[l].code + off);
+      if (l < nres) lq[l] = lqn[l];
+    if (mt + stride < mts) fetch(mt + stride);
     int k0[4], k1[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -903,8 +915,9 @@ int qnn_chain_epilogue(const uint8_t* bncode, int n, int ho, int wo, int c, cons
   QNN_REQUIRE(M < ((int64_t)1 << 31), "n * ho * wo >= 2^31");
   const int64_t mts = (M + 31) / 32;
   const int ct = (c + 31) / 32;
-  // about 8 blocks per CU over the channel tiles, each walking pixel tiles four at a time
-  const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(cdiv(mts, 4), cdiv(256 * 8, ct)));
+  // one resident round: about 4 blocks per CU (<= 128 VGPRs) over the channel tiles, each
+  // walking pixel tiles four at a time (a second, partial round of blocks would run at low occupancy)
+  const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(cdiv(mts, 4), (256 * 4) / ct));
   const dim3 grid((unsigned)gx, (unsigned)ct);
   const int64_t step = 32 * 4 * gx;  // pixels between a wave's tiles
   const int dx = (int)(step % wo), rows = (int)(step / wo), dy = rows % ho, dn = rows / ho;
