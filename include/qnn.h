@@ -431,6 +431,19 @@ int qnn_dwconv_fused_lut(const int8_t* x, int n, int h, int w, int pad, int hp, 
 int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* out_f32,
                       const qnn_code_out* code0, qnn_stream_t stream);
 
+/* The drop-in QConv2d forward (quantize.py:314-349) for the shapes the int8 MFMA path does not
+ * take -- dilation != 1, grouped convs other than depthwise, unequal or 'same' padding -- from the
+ * module's fp32 NCHW input: F.conv2d(input_, qweight, qbias, stride, padding, dilation, groups) on
+ * the fake-quantized input (quantized on the fly with the QuantMeasure range neg_min / xmin /
+ * scale / qmax) and w_hat, the fake-quantized weight [cout][c / groups][kh][kw] (qnn_pack_weight_i8's
+ * w_hat); products summed in fp64, rounded once, + bias (the quantized bias, nullable).  Zero
+ * padding pad_top / pad_left before the first row / column (the bottom / right padding follows from
+ * ho / wo).  A correctness path (one thread per output), not a tuned kernel. */
+int qnn_qconv2d_generic_fwd(const float* x, int n, int c, int h, int w, float neg_min, float xmin, float scale,
+                            float qmax, const float* w_hat, int cout, int groups, int kh, int kw, int sh, int sw,
+                            int pad_top, int pad_left, int dil_h, int dil_w, int ho, int wo, const float* bias,
+                            float* y, qnn_stream_t stream);
+
 /* The residual-chain tail of a ResNet block's last conv as a launch of its own (the "split"
  * general epilogue; resnet_quantized.py:60-68 / :105-113 after the conv): bncode holds that
  * conv's RangeBN input codes [n*ho*wo][c] in the byte C-tile layout (qnn_qconv2d_fwd with

@@ -312,6 +312,49 @@ __global__ __launch_bounds__(256) void quantize_s2d_rows_kernel(const float* __r
     *reinterpret_cast<int4*>(z + (int64_t)n * hz * wz * 16 + 16 * threadIdx.x) = make_int4(0, 0, 0, 0);
 }
 
+// ------------------------------------------------------------------ generic drop-in conv
+// F.conv2d(input_, qweight, qbias, stride, padding, dilation, groups) of QConv2d.forward
+// (quantize.py:342-344) for the shapes the int8 MFMA path does not take: dilation != 1, grouped
+// convs other than depthwise, unequal / string ('same', 'valid') padding.  A correctness path, not
+// a tuned one: one thread per output, the input fake-quantized on the fly with the quantizer's own
+// op order (quant_code -> dequant, quantize.py:89-100), the products of the fake-quantized operands
+// summed in fp64 and rounded once, then + the quantized bias (as the reference's conv adds it).
+__global__ __launch_bounds__(256) void qconv_generic_kernel(const float* __restrict__ x, int n, int c, int h, int w,
+                                                            float neg_min, float xmin, float scale, float qmax,
+                                                            const float* __restrict__ w_hat, int cout, int groups,
+                                                            int kh, int kw, int sh, int sw, int pt, int pl, int dh,
+                                                            int dw, int ho, int wo, const float* __restrict__ bias,
+                                                            float* __restrict__ y) {
+  const int cin_g = c / groups, cout_g = cout / groups;
+  const int64_t total = (int64_t)n * cout * ho * wo;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % wo);
+    int64_t r = i / wo;
+    const int oy = (int)(r % ho);
+    r /= ho;
+    const int co = (int)(r % cout), img = (int)(r / cout);
+    const int g = co / cout_g;
+    const float* wp = w_hat + (int64_t)co * cin_g * kh * kw;
+    double acc = 0.0;
+    for (int ci = 0; ci < cin_g; ++ci) {
+      const float* xp = x + ((int64_t)img * c + g * cin_g + ci) * h * w;
+      for (int ky = 0; ky < kh; ++ky) {
+        const int iy = oy * sh - pt + ky * dh;
+        if (iy < 0 || iy >= h) continue;
+        for (int kx = 0; kx < kw; ++kx) {
+          const int ix = ox * sw - pl + kx * dw;
+          if (ix < 0 || ix >= w) continue;
+          const float xq = fake_quant(xp[(int64_t)iy * w + ix], neg_min, xmin, scale, qmax);
+          acc += (double)xq * (double)wp[(ci * kh + ky) * kw + kx];
+        }
+      }
+    }
+    float v = (float)acc;
+    if (bias) v = v + bias[co];
+    y[i] = v;
+  }
+}
+
 // ------------------------------------------------------------------ gradient quantizer
 // quantize.py:76-97 with enforce_true_zero (the binding of UniformQuantizeGrad.backward):
 // the reference's in-place op order, one element per lane, four per thread
@@ -655,6 +698,25 @@ int qnn_quantize_nchw_to_nhwc8(const float* x, int8_t* q, int n, int c, int h, i
   hipLaunchKernelGGL(quantize_nchw_nhwc8_kernel, dim3(grid_for(work > 0 ? work : 1, 256)), dim3(256), 0,
                      (hipStream_t)stream, x, q, n, c, h, w, pad, cp, neg_min, scale, qmax);
   QNN_LAUNCH_CHECK("qnn_quantize_nchw_to_nhwc8");
+  return QNN_OK;
+}
+
+int qnn_qconv2d_generic_fwd(const float* x, int n, int c, int h, int w, float neg_min, float xmin, float scale,
+                            float qmax, const float* w_hat, int cout, int groups, int kh, int kw, int sh, int sw,
+                            int pad_top, int pad_left, int dil_h, int dil_w, int ho, int wo, const float* bias,
+                            float* y, qnn_stream_t stream) {
+  QNN_REQUIRE(n >= 0 && c > 0 && h > 0 && w > 0 && cout > 0 && groups > 0 && c % groups == 0 && cout % groups == 0 &&
+                  kh > 0 && kw > 0 && sh > 0 && sw > 0 && pad_top >= 0 && pad_left >= 0 && dil_h > 0 && dil_w > 0 &&
+                  ho > 0 && wo > 0,
+              "bad shape");
+  QNN_REQUIRE(scale > 0.f, "scale must be > 0");
+  if (n == 0) return QNN_OK;
+  QNN_REQUIRE(x && w_hat && y, "null pointer");
+  const int64_t total = (int64_t)n * cout * ho * wo;
+  hipLaunchKernelGGL(qconv_generic_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, x, n, c, h,
+                     w, neg_min, xmin, scale, qmax, w_hat, cout, groups, kh, kw, sh, sw, pad_top, pad_left, dil_h,
+                     dil_w, ho, wo, bias, y);
+  QNN_LAUNCH_CHECK("qnn_qconv2d_generic_fwd");
   return QNN_OK;
 }
 

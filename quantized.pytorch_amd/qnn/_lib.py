@@ -99,6 +99,9 @@ SIGNATURES = {
     "qnn_avgpool_quant": [c_ptr, c_int, c_int, c_int, c_int, c_ptr, _PC, c_ptr],
     "qnn_bn_code_lut": [_PB, c_int, c_int, _PC, c_ptr, c_ptr],
     "qnn_chain_epilogue": [c_ptr, c_int, c_int, c_int, c_int, ctypes.POINTER(Epilogue), c_ptr],
+    "qnn_qconv2d_generic_fwd": [c_ptr, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_ptr, c_int,
+                                c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                                c_ptr, c_ptr],
     "qnn_comm_unique_id": [c_ptr, ctypes.c_size_t],
     "qnn_comm_init": [c_int, c_int, c_ptr],
     "qnn_gather_f32": [c_ptr, c_ptr, ctypes.c_size_t, c_int, c_ptr],

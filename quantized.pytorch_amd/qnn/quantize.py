@@ -749,15 +749,15 @@ class QConv2d(nn.Conv2d, QuantNode, _QLayerMixin):
         if not self.enable_quant:
             return F.conv2d(input, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
         _require_device(input, "QConv2d")
-        if tuple(self.dilation) != (1, 1):
-            raise NotImplementedError("qnn: dilation != 1 is not on the int8 path")
-        if self.padding_mode != "zeros" or isinstance(self.padding, str):
-            raise NotImplementedError("qnn: only explicit zero padding is on the int8 path")
-        if self.groups != 1 and not self._is_depthwise():
-            raise NotImplementedError("qnn: grouped conv other than depthwise is not on the int8 path")
+        # the reference calls F.conv2d(input_, qweight, qbias, stride, padding, dilation, groups)
+        # (quantize.py:342-344): padding_mode is never applied (zeros), string padding is F.conv2d's
+        generic = (tuple(self.dilation) != (1, 1) or isinstance(self.padding, str) or
+                   self.padding[0] != self.padding[1] or (self.groups != 1 and not self._is_depthwise()))
 
         def fwd(x):
             x = x.contiguous()
+            if generic:
+                return self._generic_forward(x, rng)
             if self._is_depthwise():
                 return self._dw_forward(x, rng)
             return self._int8_forward(x, rng, self.stride, self.padding)
@@ -766,6 +766,40 @@ class QConv2d(nn.Conv2d, QuantNode, _QLayerMixin):
             return _QLayerTrain.apply(input, self.weight, self.bias, self, rng, fwd)
         with torch.no_grad():
             return fwd(input.detach())
+
+    def _generic_forward(self, x, rng):
+        """Dilated, grouped (other than depthwise) or unevenly / 'same'-padded QConv2d: the
+        generic device conv (qnn_qconv2d_generic_fwd) on the fake-quantized operands."""
+        pk = self._pack(depthwise=True)  # (its w_hat: the fake-quantized weight, any cin_g)
+        N, C, H, W = x.shape
+        cout, cin_g, kh, kw = self._weight4().shape
+        if C != cin_g * self.groups:
+            raise RuntimeError(f"qnn: expected {cin_g * self.groups} input channels, got {C}")
+        sh, sw = self.stride
+        dh, dw = self.dilation
+        if isinstance(self.padding, str):
+            if self.padding == "valid":
+                pt = pb = pl = pr = 0
+            else:  # 'same' (stride 1): F.conv2d puts the odd extra row / column at the bottom / right
+                if (sh, sw) != (1, 1):
+                    raise ValueError("padding='same' is not supported for strided convolutions")
+                th, tw = dh * (kh - 1), dw * (kw - 1)
+                pt, pl = th // 2, tw // 2
+                pb, pr = th - pt, tw - pl
+        else:
+            pt = pb = self.padding[0]
+            pl = pr = self.padding[1]
+        Ho = (H + pt + pb - dh * (kh - 1) - 1) // sh + 1
+        Wo = (W + pl + pr - dw * (kw - 1) - 1) // sw + 1
+        if Ho <= 0 or Wo <= 0:
+            raise RuntimeError("qnn: output size is empty")
+        mn, mx = rng
+        s = float_scale(mn, mx, self.num_bits)
+        y = torch.empty((N, cout, Ho, Wo), dtype=torch.float32, device=x.device)
+        _lib.call("qnn_qconv2d_generic_fwd", _lib.ptr(x), N, C, H, W, -float(mn), float(mn), s, _qmax(self.num_bits),
+                  _lib.ptr(pk.w_hat), cout, self.groups, kh, kw, sh, sw, pt, pl, dh, dw, Ho, Wo, _lib.ptr(pk.qbias),
+                  _lib.ptr(y), _lib.stream_of(x))
+        return y
 
     def _dw_forward(self, x, rng):
         pk = self._pack(depthwise=True)
