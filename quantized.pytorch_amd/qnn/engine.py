@@ -100,11 +100,13 @@ class Engine:
         split_chain: each ResNet block's last conv writes only its RangeBN input codes and the
         residual-chain tail (RangeBN, + the block input, ReLU, the consumers' codes) runs as a
         launch of its own (qnn_chain_epilogue: no MFMA, full occupancy, packed FP32) instead of
-        in the conv's epilogue; bitwise the same outputs.  None = QNN_ENGINE_SPLIT_CHAIN."""
+        in the conv's epilogue; bitwise the same outputs.  True: every block; False: none; "auto"
+        (the default, QNN_ENGINE_SPLIT_CHAIN=auto|1|0): only where it measured faster
+        (`_split_pays`, profiles/r6_split_chain_vs_fused.txt)."""
         self.fuse_stem_pool = fuse_stem_pool
         if split_chain is None:
-            split_chain = os.environ.get("QNN_ENGINE_SPLIT_CHAIN", "0") == "1"
-        self.split_chain = bool(split_chain)
+            split_chain = {"1": True, "0": False}.get(os.environ.get("QNN_ENGINE_SPLIT_CHAIN", "auto"), "auto")
+        self.split_chain = split_chain if split_chain == "auto" else bool(split_chain)
         if branches is None:
             branches = os.environ.get("QNN_ENGINE_BRANCHES", "0") == "1"
         self.branches = bool(branches)
@@ -343,12 +345,25 @@ class Engine:
                 setattr(e, f"code{k}_{f}", getattr(co, f))
             setattr(e, f"out_code{k}", co.ptr)
 
+    def _split_pays(self, conv, Ho, Wo, outs, out_f32):
+        """Where the split chain epilogue measured faster than the fused one
+        (profiles/r6_split_chain_vs_fused.txt, ResNet-50 b256): a 1x1 conv (its contraction small
+        beside its epilogue) writing >= 1e8 outputs to a single code consumer and no fp32 map --
+        ResNet-50's layer-1 / layer-2 expand convs inside a stage (-4 to -24 us each).  A block
+        feeding two consumers or an fp32 checkpoint, the deeper layers and every ResNet-18 block
+        measured slower split.  A shape rule, so every rank of a sharded engine plans the same."""
+        k1 = tuple(conv.kernel_size) == (1, 1)
+        return k1 and len(outs) == 1 and out_f32 is None and self.N * Ho * Wo * conv.out_channels >= 100_000_000
+
     def _conv_chain(self, conv, src, H, W, Ho, Wo, bn, chain, outs, out_f32, out_bncode):
         """A block's last conv: RangeBN, + the block input (chain), ReLU, the consumers' codes, the
         fp32 map (out_f32) and its own RangeBN codes as the next chain link (out_bncode) -- fused in
         the conv's general epilogue, or (split_chain) as the conv's RangeBN codes and one
         qnn_chain_epilogue launch over them (resnet_quantized.py:60-68 / :105-113)."""
-        if not self.split_chain:
+        split = self.split_chain
+        if split == "auto":
+            split = self._split_pays(conv, Ho, Wo, outs, out_f32)
+        if not split:
             self._conv(conv, src, H, W, bn=bn, chain=chain, relu=True, outs=outs, out_f32=out_f32,
                        out_bncode=out_bncode, bncode_tiled=True)
             return
