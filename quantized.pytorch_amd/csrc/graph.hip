@@ -532,7 +532,7 @@ __global__ __launch_bounds__(64) void avgpool_quant_kernel(const float* __restri
 // AvgPool2d), divides by hw, and the codes go out four channels per thread.  hw <= 128.
 __global__ __launch_bounds__(64) void avgpool_tiled_kernel(const float* __restrict__ x, int n, int hw, int c,
                                                            float* out_f32, qnn_code_out c0) {
-  __shared__ float s_x[128 * 64];
+  extern __shared__ float s_x[];  // [hw][64]
   const int img = blockIdx.y, cb = blockIdx.x * 64, lane = threadIdx.x;
   const int ct = (c + 31) >> 5;
   const int64_t mlo = (int64_t)img * hw, mhi = mlo + hw;
@@ -552,6 +552,7 @@ __global__ __launch_bounds__(64) void avgpool_tiled_kernel(const float* __restri
   }
   __syncthreads();
   float sum = 0.f;
+#pragma unroll 8
   for (int t = 0; t < hw; ++t) sum = sum + s_x[t * 64 + lane];
   const float val = sum / (float)hw;
   const int ch = cb + lane;
@@ -1009,7 +1010,7 @@ int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* 
   const qnn_code_out c0 = code0 ? *code0 : none_code();
   QNN_REQUIRE(n < 65536, "batch >= 65536");
   if (x_tiled && hw <= 128 && (((uintptr_t)x) & 15) == 0)
-    hipLaunchKernelGGL(avgpool_tiled_kernel, dim3((unsigned)cdiv(c, 64), (unsigned)n), dim3(64), 0,
+    hipLaunchKernelGGL(avgpool_tiled_kernel, dim3((unsigned)cdiv(c, 64), (unsigned)n), dim3(64), hw * 64 * 4,
                        (hipStream_t)stream, x, n, hw, c, out_f32, c0);
   else
     hipLaunchKernelGGL(avgpool_quant_kernel, dim3((unsigned)cdiv(c / 4, 64), (unsigned)n), dim3(64), 0,

@@ -100,12 +100,12 @@ class Engine:
         split_chain: each ResNet block's last conv writes only its RangeBN input codes and the
         residual-chain tail (RangeBN, + the block input, ReLU, the consumers' codes) runs as a
         launch of its own (qnn_chain_epilogue: no MFMA, full occupancy, packed FP32) instead of
-        in the conv's epilogue; bitwise the same outputs.  True: every block; False: none; "auto"
-        (the default, QNN_ENGINE_SPLIT_CHAIN=auto|1|0): only where it measured faster
-        (`_split_pays`, profiles/r6_split_chain_vs_fused.txt)."""
+        in the conv's epilogue; bitwise the same outputs.  True: every block; False (the default,
+        QNN_ENGINE_SPLIT_CHAIN=0|1|auto): none; "auto": the blocks `_split_pays` names -- measured
+        1 % slower than none on ResNet-50 b256 on one box (profiles/r6_split_chain_ab.txt), so off."""
         self.fuse_stem_pool = fuse_stem_pool
         if split_chain is None:
-            split_chain = {"1": True, "0": False}.get(os.environ.get("QNN_ENGINE_SPLIT_CHAIN", "auto"), "auto")
+            split_chain = {"1": True, "auto": "auto"}.get(os.environ.get("QNN_ENGINE_SPLIT_CHAIN", "0"), False)
         self.split_chain = split_chain if split_chain == "auto" else bool(split_chain)
         if branches is None:
             branches = os.environ.get("QNN_ENGINE_BRANCHES", "0") == "1"
@@ -346,8 +346,9 @@ class Engine:
             setattr(e, f"out_code{k}", co.ptr)
 
     def _split_pays(self, conv, Ho, Wo, outs, out_f32):
-        """Where the split chain epilogue measured faster than the fused one
-        (profiles/r6_split_chain_vs_fused.txt, ResNet-50 b256): a 1x1 conv (its contraction small
+        """Where the per-launch traces suggested the split chain epilogue is faster than the fused
+        one (profiles/r6_split_chain_vs_fused.txt, two boxes; a same-box A/B then measured the rule
+        1 % slower overall, profiles/r6_split_chain_ab.txt): a 1x1 conv (its contraction small
         beside its epilogue) writing >= 1e8 outputs to a single code consumer and no fp32 map --
         ResNet-50's layer-1 / layer-2 expand convs inside a stage (-4 to -24 us each).  A block
         feeding two consumers or an fp32 checkpoint, the deeper layers and every ResNet-18 block
