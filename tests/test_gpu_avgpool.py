@@ -1,5 +1,5 @@
 """qnn_avgpool_quant (resnet_quantized.py:153, mobilenet_quantized.py:157): the engine's global
-average pool, from an NHWC map and from a C-tile map (the LDS-staged kernel), bitwise torch's
+average pool, from an NHWC map and from a C-tile map, bitwise torch's
 AvgPool2d on the device, and the classifier's input codes bitwise the quantizer's."""
 import pytest
 import torch
