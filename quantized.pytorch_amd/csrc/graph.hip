@@ -525,6 +525,49 @@ __global__ __launch_bounds__(64) void avgpool_quant_kernel(const float* __restri
   if (c0.ptr) put_code4(c0, img, 0, 0, 4 * g, val);
 }
 
+// The same mean from a C-tile map, staged through LDS so the reads are coalesced: a 64-thread
+// block owns one image and 64 channels; the C-tile stores 32 pixels x 8 channels contiguously
+// (1 KiB, one float4 per lane), so each load instruction reads one such piece, scattered into LDS
+// as [tap][64 channels] (row stride 68 floats: conflict-free 16-byte writes and reads); then thread = channel sums its taps in row-major order (s = s + v, as
+// AvgPool2d), divides by hw, and the codes go out four channels per thread.  hw <= 128.
+__global__ __launch_bounds__(64) void avgpool_tiled_kernel(const float* __restrict__ x, int n, int hw, int c,
+                                                           float* out_f32, qnn_code_out c0) {
+  extern __shared__ float s_x[];  // [hw][RS]: rows padded to 68 floats (the 32 pixels of a piece in distinct banks)
+  const int img = blockIdx.y, cb = blockIdx.x * 64, lane = threadIdx.x;
+  const int ct = (c + 31) >> 5;
+  const int64_t mlo = (int64_t)img * hw, mhi = mlo + hw;
+  const int64_t mt0 = mlo >> 5, mt1 = (mhi - 1) >> 5;
+  const int mi = lane & 31, h = lane >> 5;
+  for (int64_t mt = mt0; mt <= mt1; ++mt) {
+    const int64_t m = mt * 32 + mi;
+    const bool in = m >= mlo && m < mhi;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // (channel tile, group of 8) pieces of this block's 64 channels
+      const int ctile = (cb >> 5) + (k >> 2), g = k & 3;
+      if (ctile >= ct) continue;
+      const float4 v = *reinterpret_cast<const float4*>(x + (((mt * ct + ctile) * 4 + g) << 8) + lane * 4);
+      const int cl = (k >> 2) * 32 + 8 * g + 4 * h;  // local channel of v.x
+      if (in) *reinterpret_cast<float4*>(s_x + (m - mlo) * 68 + cl) = v;
+    }
+  }
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll 8
+  for (int t = 0; t < hw; ++t) sum = sum + s_x[t * 68 + lane];
+  const float val = sum / (float)hw;
+  const int ch = cb + lane;
+  if (out_f32 && ch < c) out_f32[(int64_t)img * c + ch] = val;
+  if (c0.ptr) {
+    __syncthreads();
+    s_x[lane] = val;
+    __syncthreads();
+    if (lane < 16 && cb + 4 * lane < c) {
+      const float v4[4] = {s_x[4 * lane], s_x[4 * lane + 1], s_x[4 * lane + 2], s_x[4 * lane + 3]};
+      put_code4(c0, img, 0, 0, cb + 4 * lane, v4);
+    }
+  }
+}
+
 static int grid_for(int64_t work) {
   int64_t g = cdiv(work, 256);
   if (g > 256 * 32) g = 256 * 32;
@@ -966,8 +1009,12 @@ int qnn_avgpool_quant(const float* x, int n, int hw, int c, int x_tiled, float* 
   QNN_REQUIRE(x, "null input");
   const qnn_code_out c0 = code0 ? *code0 : none_code();
   QNN_REQUIRE(n < 65536, "batch >= 65536");
-  hipLaunchKernelGGL(avgpool_quant_kernel, dim3((unsigned)cdiv(c / 4, 64), (unsigned)n), dim3(64), 0,
-                     (hipStream_t)stream, x, n, hw, c, x_tiled, out_f32, c0);
+  if (x_tiled && hw <= 128 && (((uintptr_t)x) & 15) == 0)
+    hipLaunchKernelGGL(avgpool_tiled_kernel, dim3((unsigned)cdiv(c, 64), (unsigned)n), dim3(64), hw * 68 * 4,
+                       (hipStream_t)stream, x, n, hw, c, out_f32, c0);
+  else
+    hipLaunchKernelGGL(avgpool_quant_kernel, dim3((unsigned)cdiv(c / 4, 64), (unsigned)n), dim3(64), 0,
+                       (hipStream_t)stream, x, n, hw, c, x_tiled, out_f32, c0);
   QNN_LAUNCH_CHECK("qnn_avgpool_quant");
   return QNN_OK;
 }
