@@ -261,20 +261,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
   const int sl = blk % nsl, pblk = blk / nsl;   // channel slice, pixel block
   const int cbl = CPT * tc, cb = sl * cs + cbl;  // this thread's channels: local, global
   extern __shared__ __attribute__((aligned(16))) int8_t s_lut[];
-  if constexpr (LUT) {
-    // the slice's code table, transposed into LDS as [code][cs]: a lookup's bank then follows
-    // the lane's channel instead of the (random) code, so the 32 lanes of a group, which hold
-    // distinct channels, read distinct banks ([cs][256] made ~70 % of the lookups' LDS cycles
-    // bank conflicts, PMC).  Staged before any thread may leave; channel fastest across lanes,
-    // so each byte store of a wave is also conflict-free.
+  if constexpr (LUT) {  // the slice's code table [cs][256], before any thread may leave
     const int8_t* src = lut + (size_t)sl * cs * 256;
-    for (int i = threadIdx.x; i < cs * 16; i += 256) {
-      const int ch = i % cs, qc = i / cs;
-      const uint4 v = *reinterpret_cast<const uint4*>(src + ch * 256 + 16 * qc);
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 16; ++k) s_lut[(16 * qc + k) * cs + ch] = (int8_t)(wv[k >> 2] >> (8 * (k & 3)));
-    }
+    for (int i = 16 * threadIdx.x; i < cs * 256; i += 16 * 256)
+      *reinterpret_cast<uint4*>(s_lut + i) = *reinterpret_cast<const uint4*>(src + i);
     __syncthreads();
   }
   if (tp >= per_blk) return;  // cs/CPT not a divisor of 256: idle tail threads
@@ -430,8 +420,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QNN_DW_WPE)
             const f2 y = bias ? acc[i][j][p] + bi[p] : acc[i][j][p];
             const f2 m = qclamp2(y, bnp) + MAGIC_U8;
             const int ch = cbl + 2 * p;
-            const uint32_t b0 = (uint8_t)s_lut[(__float_as_uint(m.x) & 255u) * cs + ch];
-            const uint32_t b1 = (uint8_t)s_lut[(__float_as_uint(m.y) & 255u) * cs + ch + 1];
+            const uint32_t b0 = (uint8_t)s_lut[ch * 256 + (__float_as_uint(m.x) & 255u)];
+            const uint32_t b1 = (uint8_t)s_lut[(ch + 1) * 256 + (__float_as_uint(m.y) & 255u)];
             wd |= (b0 | (b1 << 8)) << (16 * (p - p2));
           }
           cw[p2 / 2] = wd;
