@@ -206,8 +206,14 @@ def test_sharded_engine_world2_device(gpu, tmp_path):
             for k in names:
                 a, b = getattr(m0, k), getattr(m1, k)
                 v = (a.double() * w[0] + b.double() * w[1]) / (w[0] + w[1])
-                a.copy_(v)
-                assert torch.equal(got["state"][n + "." + k if n else k], a.cpu()), f"merged {n}.{k}"
+                # the per-shard statistics recomputed in this process agree with the ranks' to the
+                # device reduction's last bits (its fp64 partial sums are added in arrival order),
+                # so the merge is checked to 1e-5 here and the engine below runs the ranks' own
+                # merged state, bitwise
+                ranks = got["state"][n + "." + k if n else k]
+                rel = ((ranks.double() - v.cpu()).abs() / v.cpu().abs().clamp_min(1e-30)).max().item()
+                assert torch.allclose(ranks.double(), v.cpu(), rtol=1e-5, atol=1e-12), f"merged {n}.{k}: rel {rel:.3g}"
+                a.copy_(ranks.to(a.device))
     eng = Engine(merged, batch=GB_EVAL)
     ref = eng(synthetic.input_batch((GB_EVAL, 3, 32, 32), 600).to(gpu)).clone().cpu()
     assert got["logits"].shape == ref.shape
