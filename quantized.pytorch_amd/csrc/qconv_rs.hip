@@ -34,7 +34,7 @@ __device__ unsigned long long qnn_rs_stamps[1 << 18];
 // LATE: chunk 1 and the epilogue data issued after chunk 0's barrier instead of at kernel start
 // (their issue then stays out of chunk 0's wait; the first in-loop weight wait covers them)
 template <class C, int EK, int H, int LATE>
-__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4))) void qconv_rs_kernel(
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * C::W / 4))) void qconv_rs_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
   constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
   constexpr int CPL = 2 * H;  // planes per chunk
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::W / 4)
   // (chunk 1's pieces and the epilogue data stay in flight: the first in-loop weight wait
   // covers them)
   if (LATE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * TM) : "memory");
-  else wait_vmcnt_rt((DA - 1) * TM + (nchunk > 1 ? CPL : 0) + njobs);
+  else wait_vmcnt_rt((DA - 1) * TM + (nchunk > 1 ? ppc : 0) + njobs);
 #if QNN_STAMP
   RB_TS(tb);
 #endif
@@ -483,7 +483,7 @@ static int rs_plan(const Params& p, Params& q, Geo& g) {
   const int cpl = 2 * H, spc = H * p.taps;
   // one DMA range per wave and plane (the chunk-0 wait counts pieces at compile time); chunk
   // boundaries on whole DA-step groups; one band pixel and one output pixel per thread
-  if (g.npl % cpl || spc % C::DA || g.ppp > C::W || g.nbp > C::NT || g.npx > C::NT) return -1;
+  if (g.npl % cpl || spc % C::DA || g.nbp > C::NT || g.npx > C::NT) return -1;
   if (p.d.ho > 255 || p.d.wo > 255 || p.d.n > 65535) return -1;  // (the pixel table's packed coordinates)
   q = p;
   const int box = 16 * g.npx;  // the pixel table (int4 per output pixel)
@@ -492,8 +492,16 @@ static int rs_plan(const Params& p, Params& q, Geo& g) {
   // (the code-table path addresses code0 with 32-bit pixel offsets)
   const bool off32 = p.e.out_code0 == nullptr ||
                      (int64_t)p.d.n * p.e.code0_hp * p.e.code0_wp * p.e.code0_cp < ((int64_t)1 << 31);
-  if (EK == EK_LUT && off32 && main + box + epi + 256 * C::BM <= LDS_MAX) g.lut = 1, epi += 256 * C::BM;
-  if (main + box + epi > LDS_MAX) return -1;
+  // BPC > 1: co-resident blocks (one's start-up and epilogue under the other's K loop), so the
+  // block fits LDS_MAX / BPC and leaves the code table out (the epilogue evaluates the chain)
+  const int lds_max = LDS_MAX / C::BPC;
+  if (EK == EK_LUT && C::BPC == 1 && off32 && main + box + epi + 256 * C::BM <= lds_max) g.lut = 1, epi += 256 * C::BM;
+  if (main + box + epi > lds_max) return -1;
+  // the chunk-0 wait counts this wave's DMAs still allowed in flight: chunk 1's pieces, the
+  // epilogue jobs and the first weights, within vmcnt's 6 bits
+  const int npr = (g.ppp + C::W - 1) / C::W, cw = 16 * C::TM, vj = (cw + 63) / 64;
+  const int narr = ((EK != EK_NCHW && p.e.bn_mean) ? 7 : 3) + p.e.nclass + (EK == EK_GEN ? 4 * p.e.nres : 0);
+  if (npr * cpl + (C::DA - 1) * C::TM + narr * vj + (g.lut ? cw / 4 : 0) > 63) return -1;
   q.epi_early = 1, q.scr_off = main, q.epi_off = main + box;
   return main + box + epi;
 }
@@ -553,16 +561,17 @@ static bool rs_ok_h(const Params& p) {
 //   4   256 x 224               8 (64 x 112)    128 ch     at start        each band fragment feeds 4 MFMAs
 //   5   256 x 112               8 (32 x 112)    128 ch     at start        half 14x14 images (ResNet-18 layer 3, b128)
 //   6   256 x 112               8 (32 x 112)    64 ch      after chunk 0
-//   7   128 x 112               8 (16 x 112)    128 ch     at start        2 images of 7x7 on 512 channels (layer 4, b128)
+//   7   128 x 208               4 (32 x 208)    128 ch     at start        two co-resident blocks per CU (no code
+//                                                                            table in LDS), 14x14 images
 using S0 = Cfg<8, 1, 2, 13, 3, 1>;
 using S2 = Cfg<4, 2, 4, 7, 3, 1>;
 using S3 = Cfg<8, 1, 2, 7, 3, 1>;
-using S5 = Cfg<8, 1, 1, 7, 4, 1>;
+using S6 = Cfg<4, 1, 2, 13, 3, 2>;
 constexpr int NS = 8;
 static const Info SINFO[NS] = {
     {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f},
     {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f}, {256, 112, 8, 1, 14, 1.10f},
-    {256, 112, 8, 1, 14, 1.10f}, {128, 112, 8, 1, 7, 0.80f},
+    {256, 112, 8, 1, 14, 1.10f}, {128, 208, 4, 2, 26, 1.55f},
 };
 
 template <int K, class F>
@@ -577,7 +586,7 @@ static auto rs_cfg(F&& f) {
   else if constexpr (K == 4) return f(S2{}, I2{}, I0{});
   else if constexpr (K == 5) return f(S3{}, I2{}, I0{});
   else if constexpr (K == 6) return f(S3{}, I1{}, I1{});
-  else return f(S5{}, I2{}, I0{});
+  else return f(S6{}, I2{}, I0{});
 }
 
 template <int K>
