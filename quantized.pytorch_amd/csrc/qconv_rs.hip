@@ -561,17 +561,16 @@ static bool rs_ok_h(const Params& p) {
 //   4   256 x 224               8 (64 x 112)    128 ch     at start        each band fragment feeds 4 MFMAs
 //   5   256 x 112               8 (32 x 112)    128 ch     at start        half 14x14 images (ResNet-18 layer 3, b128)
 //   6   256 x 112               8 (32 x 112)    64 ch      after chunk 0
-//   7   128 x 208               4 (32 x 208)    128 ch     at start        two co-resident blocks per CU (no code
-//                                                                            table in LDS), 14x14 images
+//   7   128 x 112               8 (16 x 112)    128 ch     at start        2 images of 7x7 on 512 channels (layer 4, b128)
 using S0 = Cfg<8, 1, 2, 13, 3, 1>;
 using S2 = Cfg<4, 2, 4, 7, 3, 1>;
 using S3 = Cfg<8, 1, 2, 7, 3, 1>;
-using S6 = Cfg<4, 1, 2, 13, 3, 2>;
+using S5 = Cfg<8, 1, 1, 7, 4, 1>;
 constexpr int NS = 8;
 static const Info SINFO[NS] = {
     {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f}, {256, 208, 8, 1, 26, 1.55f},
     {256, 208, 8, 1, 26, 1.55f}, {256, 224, 8, 1, 28, 1.55f}, {256, 112, 8, 1, 14, 1.10f},
-    {256, 112, 8, 1, 14, 1.10f}, {128, 208, 4, 2, 26, 1.55f},
+    {256, 112, 8, 1, 14, 1.10f}, {128, 112, 8, 1, 7, 0.80f},
 };
 
 template <int K, class F>
@@ -586,7 +585,7 @@ static auto rs_cfg(F&& f) {
   else if constexpr (K == 4) return f(S2{}, I2{}, I0{});
   else if constexpr (K == 5) return f(S3{}, I2{}, I0{});
   else if constexpr (K == 6) return f(S3{}, I1{}, I1{});
-  else return f(S6{}, I2{}, I0{});
+  else return f(S5{}, I2{}, I0{});
 }
 
 template <int K>
