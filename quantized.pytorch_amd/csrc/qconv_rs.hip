@@ -38,6 +38,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const Params p, const Geo g) {
   constexpr int BM = C::BM, W = C::W, TM = C::TM, TN = C::TN, DA = C::DA, NT = C::NT;
   constexpr int CPL = 2 * H;  // planes per chunk
+  static_assert(C::DA >= 1 && C::DA <= 4, "the K loop unrolls at most four weight slots per pass");
   constexpr int NPT = 1;      // band pixels / output pixels per thread (geometry: nbp, npx <= NT)
   constexpr int CW = 16 * TM;  // this wave's channels
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
