@@ -246,6 +246,7 @@ __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::BPC * 
     load_a(fa[(SL + DA - 1) % DA]);
     advance(cc);
   };
+  static_assert(DA >= 1 && DA <= 4, "the K loop unrolls at most four weight slots per pass");
 #pragma nounroll
   for (int k0 = 0; k0 < KS; k0 += DA) {
     step(std::integral_constant<int, 0>{});
